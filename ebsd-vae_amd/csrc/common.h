@@ -1,0 +1,112 @@
+// Shared device helpers for the ebsd-vae MI355X kernels (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in this library:
+//  * activations are NHWC fp32, index ((b*H + h)*W + w)*C + c;
+//  * a conv block's saved tensor is its PRE-norm output y (conv + bias); the
+//    normalised activation lrelu((y-mean)*rstd) is never written to HBM: consumers
+//    recompute it while staging their input tile (the "act source" below);
+//  * InstanceNorm statistics are float2 {mean, rstd} per (b, c);
+//  * launches never allocate, free or synchronise; every buffer is owned by the caller.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define EV_DEVINL __device__ __forceinline__
+
+namespace ev {
+
+constexpr float kSlope = 0.02f;   // LeakyReLU(0.02), latice/model.py:97,106
+constexpr float kInEps = 1e-5f;   // InstanceNorm2d default eps, latice/model.py:96,105
+
+// How a conv (or any consumer) reads its logical input at (b, h, w, c) from a source
+// tensor.  Matches the block boundaries of latice/model.py:109-148.
+enum ActMode : int {
+  ACT_RAW = 0,        // src itself, same resolution
+  ACT_NORM = 1,       // lrelu((src - mean) * rstd), same resolution (conv -> IN -> LReLU)
+  ACT_NORM_POOL = 2,  // max over 2x2 of ACT_NORM of src at 2x resolution (MaxPool2d(2,2))
+  ACT_UP = 3,         // src at half resolution, nearest x2 (UpsamplingNearest2d(2))
+  ACT_NORM_UP = 4,    // ACT_NORM of src at half resolution, nearest x2
+};
+
+EV_DEVINL float lrelu(float v) { return v > 0.f ? v : kSlope * v; }
+
+EV_DEVINL float normact(float v, float2 st) { return lrelu((v - st.x) * st.y); }
+
+EV_DEVINL float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+EV_DEVINL void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+EV_DEVINL float4 max4(float4 a, float4 b) {
+  return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
+}
+
+// 4 consecutive channels (c..c+3) of the logical input at (b,h,w); (h,w) in bounds.
+// H, W are the LOGICAL (consumer) dimensions, C the source channel count.
+EV_DEVINL float4 load_act4(const float* __restrict__ src, const float2* __restrict__ stats,
+                           int mode, int b, int h, int w, int c, int H, int W, int C) {
+  float4 v;
+  if (mode == ACT_RAW) {
+    v = ld4(src + (((size_t)b * H + h) * W + w) * C + c);
+    return v;
+  }
+  if (mode == ACT_UP || mode == ACT_NORM_UP) {
+    const int Hs = H >> 1, Ws = W >> 1;
+    v = ld4(src + (((size_t)b * Hs + (h >> 1)) * Ws + (w >> 1)) * C + c);
+    if (mode == ACT_UP) return v;
+  } else if (mode == ACT_NORM_POOL) {
+    const int Hs = H << 1, Ws = W << 1;
+    const float* p = src + (((size_t)b * Hs + 2 * h) * Ws + 2 * w) * C + c;
+    // max before normalising: x -> lrelu((x-m)*r) is monotone non-decreasing in fp32,
+    // so max(f(x_i)) == f(max(x_i)) bit for bit.
+    v = max4(max4(ld4(p), ld4(p + C)), max4(ld4(p + (size_t)Ws * C), ld4(p + (size_t)Ws * C + C)));
+  } else {  // ACT_NORM
+    v = ld4(src + (((size_t)b * H + h) * W + w) * C + c);
+  }
+  const float2* s = stats + (size_t)b * C + c;
+  float2 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+  return make_float4(normact(v.x, s0), normact(v.y, s1), normact(v.z, s2), normact(v.w, s3));
+}
+
+// single-channel variant (C == 1 sources, e.g. the input patterns)
+EV_DEVINL float load_act1(const float* __restrict__ src, const float2* __restrict__ stats,
+                          int mode, int b, int h, int w, int c, int H, int W, int C) {
+  float v;
+  if (mode == ACT_RAW) return src[(((size_t)b * H + h) * W + w) * C + c];
+  if (mode == ACT_UP || mode == ACT_NORM_UP) {
+    const int Hs = H >> 1, Ws = W >> 1;
+    v = src[(((size_t)b * Hs + (h >> 1)) * Ws + (w >> 1)) * C + c];
+    if (mode == ACT_UP) return v;
+  } else if (mode == ACT_NORM_POOL) {
+    const int Ws = W << 1, Hs = H << 1;
+    const float* p = src + (((size_t)b * Hs + 2 * h) * Ws + 2 * w) * C + c;
+    v = fmaxf(fmaxf(p[0], p[C]), fmaxf(p[(size_t)Ws * C], p[(size_t)Ws * C + C]));
+  } else {
+    v = src[(((size_t)b * H + h) * W + w) * C + c];
+  }
+  return normact(v, stats[(size_t)b * C + c]);
+}
+
+// wave64 reductions (DPP/permute via __shfl_xor; width 64)
+EV_DEVINL float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+}  // namespace ev
+
+// ---------------------------------------------------------------- host-side error plumbing
+namespace evh {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace evh
+
+#define EV_REQUIRE(cond, ...)        \
+  do {                               \
+    if (!(cond)) {                   \
+      evh::set_error(__VA_ARGS__);   \
+      return 1;                      \
+    }                                \
+  } while (0)

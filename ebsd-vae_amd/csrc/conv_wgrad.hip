@@ -1,0 +1,376 @@
+// Weight / bias gradients of the 3x3 convs (autograd's convolution_backward weight and
+// bias outputs for latice/model.py:95,102-104,148), on the fp32 MFMA
+// (v_mfma_f32_16x16x4_f32).
+//
+//   dWc[co][ci][tap] = sum_{b,p} gy[b,p,co] * act(src)[b, p + d(tap), ci]
+//   db[co]           = sum_{b,p} gy[b,p,co]
+//
+// GEMM view: M = co, N = ci, K = pixels (B*H*W, up to 4.2M), one accumulator per tap.
+// The K reduction is split over "slices" (contiguous runs of pixel tiles); each block
+// writes its slice's partial tile and ebsdvae_wgrad_reduce sums the slices in a fixed
+// order -> bitwise reproducible gradients (no float atomics).
+//
+// Per block: a co tile (32 or 64) x ci tile of 32; 2 or 4 waves, each co32 x ci16 x 9 taps
+// = 18 accumulators of 16x16 (72 regs).  Per k-step of 4 pixels: 2 A reads (gy) and 9 B
+// reads (shifted activations) feed 18 MFMAs.  LDS tiles: gy [128 px][co] with stride
+// CO_T+16 (== 16 mod 32 -> the two 16-lane pixel rows of an A fragment are bank-disjoint),
+// activation halo [(TH+2)(TW+2)][32] with stride 48 (same reason).  The activation is
+// recomputed from the producer's saved pre-norm output (InstanceNorm + LeakyReLU
+// [+ pool/upsample]) while staging, exactly as in the forward.
+#include "common.h"
+#include "../../include/ebsdvae.h"
+
+namespace ev {
+
+constexpr int WG_PT = 128;   // pixels per tile
+constexpr int WG_AS = 48;    // activation halo channel stride (32 + 16)
+
+struct WgGeom {
+  int TH, TW, NI, ntx, nty, tiles, slices, tps;
+};
+
+static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
+  g->TW = W < 32 ? W : 32;
+  if (H * g->TW >= WG_PT) {
+    g->TH = WG_PT / g->TW;
+    g->NI = 1;
+  } else {
+    g->TH = H;
+    g->NI = WG_PT / (H * W);
+    if (g->NI * H * W != WG_PT) return false;
+  }
+  if (W % g->TW || H % g->TH) return false;
+  g->ntx = W / g->TW;
+  g->nty = H / g->TH;
+  const long imgs = (B + g->NI - 1) / g->NI;
+  g->tiles = (int)(imgs * g->ntx * g->nty);
+  // aim for ~2048 blocks (slices x co tiles x ci tiles), >= 4 tiles per slice
+  const int co_t = cout == 1 ? 1 : (cout == 32 ? 1 : cout / 64);
+  const int ci_t = cin == 1 ? 1 : (cout == 1 ? 1 : cin / 32);
+  const int want = 2048 / (co_t * ci_t);
+  int tps = 4;
+  while ((g->tiles + tps - 1) / tps > (want > 1 ? want : 1)) tps *= 2;
+  g->tps = tps;
+  g->slices = (g->tiles + tps - 1) / tps;
+  return true;
+}
+
+EV_DEVINL void tile_origin(int t, const WgGeom& g, int& b0, int& y0, int& x0) {
+  const int per_img = g.ntx * g.nty;
+  const int ib = t / per_img, r = t - ib * per_img;
+  b0 = ib * g.NI;
+  y0 = (r / g.ntx) * g.TH;
+  x0 = (r % g.ntx) * g.TW;
+}
+
+// ------------------------------------------------------------------ generic (cin % 32 == 0)
+template <int NWCO>
+__global__ __launch_bounds__(NWCO * 128) void wgrad_kernel(
+    const float* __restrict__ src, const float2* __restrict__ sstats, int smode,
+    const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
+    int H, int W, int Cin, int Cout, WgGeom g) {
+  constexpr int CO_T = NWCO * 32;
+  constexpr int GS = CO_T + 16;
+  constexpr int NT = NWCO * 128;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* lg = smem;                 // [128][GS]
+  float* la = smem + WG_PT * GS;    // [halo px][48]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave % NWCO, wci = wave / NWCO;
+  const int slice = blockIdx.x, co0 = blockIdx.y * CO_T, ci0 = blockIdx.z * 32;
+  const int HP = g.TH + 2, WP = g.TW + 2, halo = g.NI * HP * WP;
+  const int l16 = lane & 15, kq = lane >> 4;
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;   // bias partial for co0 + tid (tid < CO_T), ci tile 0 only
+
+  const int t_beg = slice * g.tps;
+  const int t_end = min(t_beg + g.tps, g.tiles);
+  const int tpx = g.TH * g.TW;
+  for (int t = t_beg; t < t_end; ++t) {
+    int b0, y0, x0;
+    tile_origin(t, g, b0, y0, x0);
+    __syncthreads();
+    // gy tile: 128 px x CO_T channels
+    for (int i = tid; i < WG_PT * CO_T / 4; i += NT) {
+      const int px = i / (CO_T / 4), q = i - px * (CO_T / 4);
+      const int img = px / tpx, rem = px - img * tpx;
+      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int gb = b0 + img;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gb < B) v = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + q * 4);
+      st4(lg + px * GS + q * 4, v);
+    }
+    // activation halo: halo px x 32 channels
+    for (int i = tid; i < halo * 8; i += NT) {
+      const int pix = i >> 3, q = i & 7;
+      const int img = pix / (HP * WP), rem = pix - img * (HP * WP);
+      const int hh = rem / WP, ww = rem - hh * WP;
+      const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W)
+        v = load_act4(src, sstats, smode, gb, gh, gw, ci0 + q * 4, H, W, Cin);
+      st4(la + pix * WG_AS + q * 4, v);
+    }
+    __syncthreads();
+    if (blockIdx.z == 0 && tid < CO_T) {
+      for (int px = 0; px < WG_PT; ++px) bsum += lg[px * GS + tid];
+    }
+#pragma unroll 2
+    for (int s = 0; s < WG_PT / 4; ++s) {
+      const int px = 4 * s + kq;
+      const int img = px / tpx, rem = px - img * tpx;
+      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int hb = ((img * HP + r) * WP + c) * WG_AS + wci * 16 + l16;
+      const float a0 = lg[px * GS + wco * 32 + l16];
+      const float a1 = lg[px * GS + wco * 32 + 16 + l16];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int kh = tap / 3, kw = tap % 3;
+        const float bv = la[hb + (kh * WP + kw) * WG_AS];
+        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc[0][tap], 0, 0, 0);
+        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc[1][tap], 0, 0, 0);
+      }
+    }
+  }
+  // partial layout [slice][tap][co][ci]
+  const int ci = ci0 + wci * 16 + l16;
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wco * 32 + f * 16 + kq * 4 + r;
+        wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] = acc[f][tap][r];
+      }
+  if (blockIdx.z == 0 && tid < CO_T) bpart[(size_t)slice * Cout + co0 + tid] = bsum;
+}
+
+// ------------------------------------------------------------------ cin == 1 (first conv)
+// taps become the N dimension: B[k=px][j=tap] = x[px + d(tap)] (j < 9), 16x16x4 MFMA.
+__global__ __launch_bounds__(128) void wgrad_cin1_kernel(
+    const float* __restrict__ src, const float2* __restrict__ sstats, int smode,
+    const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
+    int H, int W, int Cout, WgGeom g) {
+  constexpr int GS = 48;  // 32 co + 16
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* lg = smem;
+  float* la = smem + WG_PT * GS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave = co half
+  const int slice = blockIdx.x;
+  const int HP = g.TH + 2, WP = g.TW + 2, halo = g.NI * HP * WP;
+  const int l16 = lane & 15, kq = lane >> 4;
+  const int tapj = l16 < 9 ? l16 : 0;
+  const int tkh = tapj / 3, tkw = tapj % 3;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  const int t_beg = slice * g.tps, t_end = min(t_beg + g.tps, g.tiles);
+  const int tpx = g.TH * g.TW;
+  for (int t = t_beg; t < t_end; ++t) {
+    int b0, y0, x0;
+    tile_origin(t, g, b0, y0, x0);
+    __syncthreads();
+    for (int i = tid; i < WG_PT * 8; i += 128) {
+      const int px = i >> 3, q = i & 7;
+      const int img = px / tpx, rem = px - img * tpx;
+      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int gb = b0 + img;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gb < B) v = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + q * 4);
+      st4(lg + px * GS + q * 4, v);
+    }
+    for (int i = tid; i < halo; i += 128) {
+      const int img = i / (HP * WP), rem = i - img * (HP * WP);
+      const int hh = rem / WP, ww = rem - hh * WP;
+      const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
+      float v = 0.f;
+      if (gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W)
+        v = load_act1(src, sstats, smode, gb, gh, gw, 0, H, W, 1);
+      la[i] = v;
+    }
+    __syncthreads();
+    if (tid < 32) {
+      for (int px = 0; px < WG_PT; ++px) bsum += lg[px * GS + tid];
+    }
+    for (int s = 0; s < WG_PT / 4; ++s) {
+      const int px = 4 * s + kq;
+      const int img = px / tpx, rem = px - img * tpx;
+      const int r = rem / g.TW, c = rem - r * g.TW;
+      const float a = lg[px * GS + wave * 16 + l16];
+      const float bv = l16 < 9 ? la[(img * HP + r + tkh) * WP + c + tkw] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+    }
+  }
+  if (l16 < 9) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = wave * 16 + kq * 4 + r;
+      wpart[((size_t)slice * 9 + l16) * Cout + co] = acc[r];   // Cin == 1
+    }
+  }
+  if (tid < 32) bpart[(size_t)slice * Cout + tid] = bsum;
+}
+
+// ------------------------------------------------------------------ cout == 1 (last conv)
+// dW[ci][tap] = sum_q g[q - d(tap)] * a[q][ci]:  A[i=tap][k=q] = shifted g (halo tile),
+// B[k=q][j=ci] = unshifted activation tile.  2 waves = ci halves (cin == 32).
+__global__ __launch_bounds__(128) void wgrad_cout1_kernel(
+    const float* __restrict__ src, const float2* __restrict__ sstats, int smode,
+    const float* __restrict__ g1, float* __restrict__ wpart, float* __restrict__ bpart, int B,
+    int H, int W, int Cin, WgGeom g) {
+  constexpr int AS = 48;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* la = smem;                  // [128 px][48]
+  float* lgh = smem + WG_PT * AS;    // g halo
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slice = blockIdx.x;
+  const int HP = g.TH + 2, WP = g.TW + 2, halo = g.NI * HP * WP;
+  const int l16 = lane & 15, kq = lane >> 4;
+  const int tapi = l16 < 9 ? l16 : 0;
+  const int tkh = tapi / 3, tkw = tapi % 3;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  const int t_beg = slice * g.tps, t_end = min(t_beg + g.tps, g.tiles);
+  const int tpx = g.TH * g.TW;
+  for (int t = t_beg; t < t_end; ++t) {
+    int b0, y0, x0;
+    tile_origin(t, g, b0, y0, x0);
+    __syncthreads();
+    for (int i = tid; i < WG_PT * 8; i += 128) {
+      const int px = i >> 3, q = i & 7;
+      const int img = px / tpx, rem = px - img * tpx;
+      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int gb = b0 + img;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gb < B) v = load_act4(src, sstats, smode, gb, y0 + r, x0 + c, q * 4, H, W, Cin);
+      st4(la + px * AS + q * 4, v);
+    }
+    for (int i = tid; i < halo; i += 128) {
+      const int img = i / (HP * WP), rem = i - img * (HP * WP);
+      const int hh = rem / WP, ww = rem - hh * WP;
+      const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
+      float v = 0.f;
+      if (gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) v = g1[((size_t)gb * H + gh) * W + gw];
+      lgh[i] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int img = 0; img < g.NI; ++img)
+        for (int r = 0; r < g.TH; ++r)
+          for (int c = 0; c < g.TW; ++c) bsum += lgh[(img * HP + r + 1) * WP + c + 1];
+    }
+    for (int s = 0; s < WG_PT / 4; ++s) {
+      const int px = 4 * s + kq;
+      const int img = px / tpx, rem = px - img * tpx;
+      const int r = rem / g.TW, c = rem - r * g.TW;
+      // g[q - d(tap)] with d(tap) = (kh-1, kw-1): halo coordinate (r+1-(kh-1), c+1-(kw-1))
+      const float a = l16 < 9 ? lgh[(img * HP + r + 2 - tkh) * WP + c + 2 - tkw] : 0.f;
+      const float bv = la[px * AS + wave * 16 + l16];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+    }
+  }
+  // acc: row i = tap = kq*4 + r, col j = ci
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int tap = kq * 4 + r;
+    if (tap < 9) wpart[((size_t)slice * 9 + tap) * Cin + wave * 16 + l16] = acc[r];  // Cout == 1
+  }
+  if (tid == 0) bpart[slice] = bsum;
+}
+
+// ------------------------------------------------------------------ slice reduction
+// thread per partial element (tap, co, ci) in [tap][co][ci] order (coalesced reads);
+// fixed-order sum over slices; scatter into the parameter-gradient layout.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ wpart, const float* __restrict__ bpart,
+                                    int S, float* __restrict__ dw, float* __restrict__ db,
+                                    int cin, int cout, int kind) {
+  const int nw = 9 * cout * cin;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nw) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < S; ++k) s += wpart[(size_t)k * nw + e];
+    const int t = e / (cout * cin), rem = e - t * (cout * cin);
+    const int co = rem / cin, ci = rem - co * cin;
+    size_t idx;
+    if (kind == 0) idx = ((size_t)co * cin + ci) * 9 + t;
+    else idx = ((size_t)ci * cout + co) * 9 + (8 - t);
+    dw[idx] = s;
+  } else if (e < nw + cout && db) {
+    const int co = e - nw;
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += bpart[(size_t)k * cout + co];
+    db[co] = s;
+  }
+}
+
+static size_t wg_lds(int variant, const WgGeom& g, int co_t) {
+  const size_t halo = (size_t)g.NI * (g.TH + 2) * (g.TW + 2);
+  if (variant == 0) return (WG_PT * (co_t + 16) + halo * WG_AS) * sizeof(float);
+  if (variant == 1) return (WG_PT * 48 + halo) * sizeof(float);
+  return (WG_PT * 48 + halo) * sizeof(float);
+}
+
+}  // namespace ev
+
+using namespace ev;
+
+extern "C" int ebsdvae_conv3x3_wgrad_slices(int B, int H, int W, int cin, int cout) {
+  WgGeom g;
+  if (!wg_geom(B, H, W, cin, cout, &g)) return -1;
+  return g.slices;
+}
+
+extern "C" int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, int src_mode,
+                                     const float* gy, float* wpart, float* bpart, int B, int H,
+                                     int W, int cin, int cout, ebsdvae_stream_t stream) {
+  WgGeom g;
+  EV_REQUIRE(src && gy && wpart && bpart && B > 0, "conv3x3_wgrad: null pointer");
+  EV_REQUIRE(src_mode >= 0 && src_mode <= 4, "conv3x3_wgrad: bad src_mode");
+  EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats, "conv3x3_wgrad: NORM needs stats");
+  EV_REQUIRE(wg_geom(B, H, W, cin, cout, &g), "conv3x3_wgrad: unsupported shape H=%d W=%d", H, W);
+  hipStream_t s = (hipStream_t)stream;
+  if (cin == 1) {
+    EV_REQUIRE(cout == 32, "conv3x3_wgrad: cin=1 needs cout=32");
+    hipLaunchKernelGGL(wgrad_cin1_kernel, dim3(g.slices), dim3(128), wg_lds(1, g, 32), s, src,
+                       (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cout, g);
+    return evh::check_launch("wgrad_cin1");
+  }
+  if (cout == 1) {
+    EV_REQUIRE(cin == 32, "conv3x3_wgrad: cout=1 needs cin=32");
+    hipLaunchKernelGGL(wgrad_cout1_kernel, dim3(g.slices), dim3(128), wg_lds(2, g, 0), s, src,
+                       (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cin, g);
+    return evh::check_launch("wgrad_cout1");
+  }
+  EV_REQUIRE(cin % 32 == 0 && (cout == 32 || cout % 64 == 0), "conv3x3_wgrad: cin=%d cout=%d unsupported",
+             cin, cout);
+  if (cout == 32) {
+    const size_t lds = wg_lds(0, g, 32);
+    auto k = wgrad_kernel<1>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3(g.slices, 1, cin / 32), dim3(128), lds, s, src,
+                       (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cin, cout, g);
+  } else {
+    const size_t lds = wg_lds(0, g, 64);
+    auto k = wgrad_kernel<2>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3(g.slices, cout / 64, cin / 32), dim3(256), lds, s, src,
+                       (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cin, cout, g);
+  }
+  return evh::check_launch("wgrad");
+}
+
+extern "C" int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
+                                    float* db, int cin, int cout, int kind,
+                                    ebsdvae_stream_t stream) {
+  EV_REQUIRE(wpart && dw && slices > 0, "wgrad_reduce: bad args");
+  const int n = 9 * cin * cout + cout;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     wpart, bpart, slices, dw, db, cin, cout, kind);
+  return evh::check_launch("wgrad_reduce");
+}

@@ -1,0 +1,120 @@
+"""ctypes binding of libebsdvae.so (the C ABI declared in include/ebsdvae.h).
+
+The library is the ONLY compute path of this package: there is no eager-PyTorch or CPU
+fallback.  If the library is missing, or a tensor is not on a ROCm device, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (loads torch's HIP runtime first; libebsdvae binds to the same one)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "EBSDVAE_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libebsdvae.so"))
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F = ctypes.c_float
+
+# name -> argtypes (restype is int unless listed in _RESTYPE)
+SIGNATURES = {
+    "ebsdvae_last_error": [],
+    "ebsdvae_version": [],
+    "ebsdvae_pack_conv_weight": [P, P, I, I, I, I, P],
+    "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_stat_tiles": [I, I, I],
+    "ebsdvae_conv3x3_cout1_fwd": [P, P, I, P, P, P, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],
+    "ebsdvae_conv3x3_wgrad_slices": [I, I, I, I, I],
+    "ebsdvae_conv3x3_wgrad": [P, P, I, P, P, P, I, I, I, I, I, P],
+    "ebsdvae_wgrad_reduce": [P, P, I, P, P, I, I, I, P],
+    "ebsdvae_in_stats_finalize": [P, P, I, I, I, I, P],
+    "ebsdvae_act_apply": [P, P, I, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_tiles": [I, I, I],
+    "ebsdvae_in_bwd_reduce": [P, I, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_finalize": [P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_apply": [P, I, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_upsample2_bwd": [P, P, I, I, I, I, P],
+    "ebsdvae_heads_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_heads_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_heads_wgrad": [P, P, P, P, P, P, P, P, P, I, I, I, P],
+    "ebsdvae_linear_fwd": [P, P, P, P, I, I, I, P],
+    "ebsdvae_linear_bwd": [P, P, P, P, P, P, I, I, I, P],
+    "ebsdvae_reparam_fwd": [P, P, P, P, P, I64, P],
+    "ebsdvae_reparam_bwd": [P, P, P, P, P, P, I64, P],
+    "ebsdvae_normal_fill": [P, I64, U64, U64, P, P],
+    "ebsdvae_vae_loss_fwd": [P, P, P, P, P, F, P, P, P, P, P, P, I, I, I, P],
+    "ebsdvae_vae_loss_bwd": [P, P, P, P, P, F, P, P, P, P, F, P, P, P, P, P, I, I, I, P],
+    "ebsdvae_adam": [P, P, P, P, P, P, I64, F, F, F, F, F, I, P],
+}
+_RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p}
+# queries that return a value rather than a status
+QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
+           "ebsdvae_in_bwd_tiles"}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes library; raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeLibraryError(
+                f"libebsdvae.so not found at {p}: build it with `python ebsd-vae_amd/build.py` "
+                "(there is no non-HIP fallback)")
+        lib = ctypes.CDLL(p)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def exported_symbols() -> list[str]:
+    return list(SIGNATURES)
+
+
+def call(name: str, *args):
+    """Invoke an entry point; nonzero status -> RuntimeError with ebsdvae_last_error()."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if name in QUERIES:
+        return rc
+    if rc != 0:
+        msg = lib.ebsdvae_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL).  Refuses non-ROCm tensors."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("the ebsd-vae MI355X path needs tensors on a ROCm device "
+                           f"(got {t.device}); there is no CPU fallback")
+    if t.dtype != torch.float32:
+        raise TypeError(f"expected float32 tensor, got {t.dtype}")
+    return t.data_ptr()
+
+
+def stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

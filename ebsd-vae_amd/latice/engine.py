@@ -1,0 +1,345 @@
+"""Launch plan of the VAE hot path over the C ABI (no autograd here).
+
+This module knows the network topology of `VariationalAutoEncoderRawData`
+(latice/model.py:109-150 in the reference) and sequences the HIP kernels of
+libebsdvae.so for the forward and the explicitly derived backward:
+
+    encoder:  10 x [conv3x3 -> InstanceNorm -> LeakyReLU], MaxPool2d after every 2nd
+    heads:    flatten(NCHW) -> mu / logvar -> std, z = mu + eps*std -> linear2 -> view
+    decoder:  5 x [Upsample -> 2 x (convT3x3 -> InstanceNorm -> LeakyReLU)] -> conv3x3(32->1)
+    loss:     BCE-with-logits + lambda * MC-KL     (latice/lightning_module.py:79-156)
+
+Every activation is NHWC fp32.  Each conv block saves only its pre-norm output y and its
+InstanceNorm statistics; all normalised / pooled / upsampled activations are recomputed
+on the fly by the consuming kernel (forward, dgrad and wgrad alike).
+
+All functions take and return torch tensors purely as device-memory handles; buffers come
+from the PyTorch caching allocator and every launch goes to the current HIP stream.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _native as N
+
+ACT_RAW, ACT_NORM, ACT_NORM_POOL, ACT_UP, ACT_NORM_UP = range(5)
+P_ID, P_POOL, P_UP = range(3)
+KIND_CONV, KIND_CONVT = 0, 1
+
+
+@dataclass(frozen=True)
+class ConvLayer:
+    name: str       # parameter prefix, e.g. "encoder.3.0"
+    kind: int       # KIND_CONV / KIND_CONVT
+    cin: int
+    cout: int
+    H: int          # output (== logical input) spatial size
+    src_mode: int   # how this conv reads its input
+    pmode: int      # how the consumer reads THIS layer's output (for the IN backward)
+
+
+@dataclass(frozen=True)
+class Plan:
+    inplanes: int
+    latent_dim: int
+    image_size: int
+    enc: tuple = field(default=())
+    dec: tuple = field(default=())
+
+    @property
+    def enc_channels(self) -> int:
+        return 4 * self.inplanes
+
+    @property
+    def enc_side(self) -> int:
+        return self.image_size // 32
+
+    @property
+    def feat(self) -> int:
+        return self.enc_channels * self.enc_side ** 2
+
+
+def build_plan(inplanes: int = 32, latent_dim: int = 16, image_size: int = 128) -> Plan:
+    """Topology of latice/model.py:109-148 (encoder idx 0,1,3,4,...; decoder idx 1,2,4,...)."""
+    p, S = inplanes, image_size
+    if S % 32 or S < 64:
+        raise ValueError(f"image_size must be a multiple of 32 and >= 64 (got {S})")
+    enc_io = [(1, p), (p, p), (p, 2 * p), (2 * p, 2 * p), (2 * p, 4 * p), (4 * p, 4 * p),
+              (4 * p, 4 * p), (4 * p, 4 * p), (4 * p, 4 * p), (4 * p, 4 * p)]
+    enc_idx = (0, 1, 3, 4, 6, 7, 9, 10, 12, 13)
+    enc = []
+    for i, ((ci, co), idx) in enumerate(zip(enc_io, enc_idx)):
+        H = S >> (i // 2)
+        if i == 0:
+            mode = ACT_RAW
+        else:
+            mode = ACT_NORM if i % 2 == 1 else ACT_NORM_POOL
+        pmode = P_POOL if i % 2 == 1 else P_ID
+        enc.append(ConvLayer(f"encoder.{idx}.0", KIND_CONV, ci, co, H, mode, pmode))
+    dec_io = [(4 * p, 4 * p), (4 * p, 4 * p), (4 * p, 4 * p), (4 * p, 4 * p), (4 * p, 4 * p),
+              (4 * p, 2 * p), (2 * p, 2 * p), (2 * p, p), (p, p)]
+    dec_idx = (1, 2, 4, 5, 7, 8, 10, 11, 13)
+    dec = []
+    for i, ((ci, co), idx) in enumerate(zip(dec_io, dec_idx)):
+        H = S >> (4 - i // 2)
+        if i == 0:
+            mode = ACT_UP
+        else:
+            mode = ACT_NORM if i % 2 == 1 else ACT_NORM_UP
+        # consumer of this layer: next layer (or the final conv, which reads ACT_NORM)
+        nxt = ACT_NORM if i == len(dec_io) - 1 else (ACT_NORM if (i + 1) % 2 == 1 else ACT_NORM_UP)
+        pmode = P_UP if nxt == ACT_NORM_UP else P_ID
+        dec.append(ConvLayer(f"decoder.{idx}.0", KIND_CONVT, ci, co, H, mode, pmode))
+    return Plan(inplanes, latent_dim, image_size, tuple(enc), tuple(dec))
+
+
+# ----------------------------------------------------------------------------- helpers
+def _empty(*shape, like):
+    return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+def pack_weight(w, layer: ConvLayer, dgrad: bool):
+    ci_, co_ = (layer.cout, layer.cin) if dgrad else (layer.cin, layer.cout)
+    out = _empty(9 * ci_ * co_, like=w)
+    N.call("ebsdvae_pack_conv_weight", N.ptr(w), N.ptr(out), layer.cin, layer.cout,
+           layer.kind, int(dgrad), N.stream())
+    return out
+
+
+def conv_forward(src, src_stats, layer: ConvLayer, w, b, B):
+    """One conv block forward: y (B,H,H,cout) pre-norm + IN stats {mean,rstd} (B,cout,2)."""
+    H = layer.H
+    wp = pack_weight(w, layer, dgrad=False)
+    y = _empty(B, H, H, layer.cout, like=w)
+    T = N.call("ebsdvae_conv3x3_stat_tiles", H, H, layer.cout)
+    part = _empty(B, T, layer.cout, 2, like=w)
+    N.call("ebsdvae_conv3x3_fwd", N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp), N.ptr(b),
+           N.ptr(y), N.ptr(part), B, H, H, layer.cin, layer.cout, N.stream())
+    st = _empty(B, layer.cout, 2, like=w)
+    N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
+           N.stream())
+    return y, st
+
+
+def in_backward(gnext, pmode, y, st):
+    """gy = d loss / d y through [pool|up] . lrelu . InstanceNorm of one block."""
+    B, H, W, C = y.shape
+    T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
+    part = _empty(B, T, C, 2, like=y)
+    s = N.stream()
+    N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(part),
+           B, H, W, C, s)
+    bst = _empty(B, C, 2, like=y)
+    N.call("ebsdvae_in_bwd_finalize", N.ptr(part), N.ptr(bst), B, C, T, H * W, s)
+    gy = torch.empty_like(y)
+    N.call("ebsdvae_in_bwd_apply", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
+           N.ptr(gy), B, H, W, C, s)
+    return gy
+
+
+def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
+    B, H, W, _ = gy.shape if gy.dim() == 4 else (*gy.shape, 1)
+    S_ = N.call("ebsdvae_conv3x3_wgrad_slices", B, H, W, cin, cout)
+    if S_ <= 0:
+        raise RuntimeError(f"wgrad: unsupported shape {H}x{W}")
+    wpart = _empty(S_, 9, cout, cin, like=gy)
+    bpart = _empty(S_, cout, like=gy)
+    s = N.stream()
+    N.call("ebsdvae_conv3x3_wgrad", N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(gy),
+           N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout, s)
+    N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db),
+           cin, cout, kind, s)
+
+
+def conv_dgrad(gy, layer: ConvLayer, w):
+    B, H, W, _ = gy.shape
+    wd = pack_weight(w, layer, dgrad=True)
+    gin = _empty(B, H, W, layer.cin, like=gy)
+    N.call("ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(wd), None, N.ptr(gin), None,
+           B, H, W, layer.cout, layer.cin, N.stream())
+    return gin
+
+
+def _grad_buf(grads, name, like):
+    if grads is not None and name in grads:
+        return grads[name]
+    return torch.empty_like(like)
+
+
+# ----------------------------------------------------------------------------- encoder
+def encoder_forward(plan: Plan, x, params):
+    """x: (B,1,S,S) fp32 (== NHWC).  Returns (enc_out NHWC (B,s,s,C), saved)."""
+    B = x.shape[0]
+    saved = {}
+    src, sst = x, None
+    for L in plan.enc:
+        y, st = conv_forward(src, sst, L, params[L.name + ".weight"], params[L.name + ".bias"], B)
+        saved[L.name] = (y, st)
+        src, sst = y, st
+    s, C = plan.enc_side, plan.enc_channels
+    out = _empty(B, s, s, C, like=x)
+    N.call("ebsdvae_act_apply", N.ptr(src), N.ptr(sst), ACT_NORM_POOL, N.ptr(out), B, s, s, C,
+           N.stream())
+    return out, saved
+
+
+def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=False):
+    """g_enc: grad of the encoder output (B,s,s,C) NHWC.  Returns (grads dict, gx or None)."""
+    out = {}
+    g_next = g_enc
+    gx = None
+    for i in reversed(range(len(plan.enc))):
+        L = plan.enc[i]
+        y, st = saved[L.name]
+        gy = in_backward(g_next, L.pmode, y, st)
+        if i == 0:
+            src, sst = x, None
+        else:
+            src, sst = saved[plan.enc[i - 1].name]
+        wn, bn = L.name + ".weight", L.name + ".bias"
+        dw = _grad_buf(grads, wn, params[wn])
+        db = _grad_buf(grads, bn, params[bn])
+        conv_wgrad(src, sst, L.src_mode, gy, L.cin, L.cout, L.kind, dw, db)
+        out[wn], out[bn] = dw, db
+        if i > 0:
+            g_next = conv_dgrad(gy, L, params[wn])
+        elif need_gx:
+            B, H, W, _ = gy.shape
+            gx = _empty(B, 1, H, W, like=gy)
+            N.call("ebsdvae_conv3x3_cout1_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(params[wn]), None,
+                   N.ptr(gx), 1, B, H, W, L.cout, N.stream())
+    return out, gx
+
+
+# ----------------------------------------------------------------------------- heads
+HEAD_NAMES = ("mu.0.weight", "mu.0.bias", "logvar.0.weight", "logvar.0.bias",
+              "linear2.0.weight", "linear2.0.bias")
+
+
+def heads_forward(plan: Plan, enc, params, eps):
+    B = enc.shape[0]
+    L, F = plan.latent_dim, plan.feat
+    s, C = plan.enc_side, plan.enc_channels
+    flat = _empty(B, F, like=enc)
+    mu = _empty(B, L, like=enc)
+    std = _empty(B, L, like=enc)
+    z = _empty(B, L, like=enc)
+    dec_in = _empty(B, s, s, C, like=enc)
+    N.call("ebsdvae_heads_fwd", N.ptr(enc), *[N.ptr(params[n]) for n in HEAD_NAMES], N.ptr(eps),
+           N.ptr(flat), N.ptr(mu), N.ptr(std), N.ptr(z), N.ptr(dec_in), B, C, s, L, N.stream())
+    return flat, mu, std, z, dec_in
+
+
+def heads_backward(plan: Plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, params, grads=None):
+    B = g_dec.shape[0]
+    L, F = plan.latent_dim, plan.feat
+    s, C = plan.enc_side, plan.enc_channels
+    g_enc = _empty(B, s, s, C, like=g_dec)
+    gs = _empty(B, 2 * L + F, like=g_dec)
+    N.call("ebsdvae_heads_bwd", N.ptr(g_dec), N.ptr(g_z), N.ptr(g_mu), N.ptr(g_std), N.ptr(std),
+           N.ptr(eps), N.ptr(params["mu.0.weight"]), N.ptr(params["logvar.0.weight"]),
+           N.ptr(params["linear2.0.weight"]), N.ptr(g_enc), N.ptr(gs), B, C, s, L, N.stream())
+    out = {n: _grad_buf(grads, n, params[n]) for n in HEAD_NAMES}
+    N.call("ebsdvae_heads_wgrad", N.ptr(flat), N.ptr(z), N.ptr(gs),
+           *[N.ptr(out[n]) for n in HEAD_NAMES], B, F, L, N.stream())
+    return g_enc, out
+
+
+# ----------------------------------------------------------------------------- decoder
+def decoder_forward(plan: Plan, dec_in, params):
+    """dec_in: (B,s,s,C) NHWC.  Returns (x_hat (B,1,S,S), saved)."""
+    B = dec_in.shape[0]
+    saved = {"__dec_in__": dec_in}
+    src, sst = dec_in, None
+    for L in plan.dec:
+        y, st = conv_forward(src, sst, L, params[L.name + ".weight"], params[L.name + ".bias"], B)
+        saved[L.name] = (y, st)
+        src, sst = y, st
+    S = plan.image_size
+    x_hat = _empty(B, 1, S, S, like=dec_in)
+    N.call("ebsdvae_conv3x3_cout1_fwd", N.ptr(src), N.ptr(sst), ACT_NORM,
+           N.ptr(params["decoder.14.weight"]), N.ptr(params["decoder.14.bias"]), N.ptr(x_hat), 0,
+           B, S, S, plan.inplanes, N.stream())
+    return x_hat, saved
+
+
+def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None):
+    """g_xhat: (B,1,S,S).  Returns (grads dict, g_dec_in (B,s,s,C) NHWC)."""
+    out = {}
+    B = g_xhat.shape[0]
+    S, p = plan.image_size, plan.inplanes
+    last = plan.dec[-1]
+    y13, st13 = saved[last.name]
+    wn, bn = "decoder.14.weight", "decoder.14.bias"
+    dw = _grad_buf(grads, wn, params[wn])
+    db = _grad_buf(grads, bn, params[bn])
+    g1 = g_xhat.reshape(B, S, S)
+    conv_wgrad(y13, st13, ACT_NORM, g1, p, 1, KIND_CONV, dw, db)
+    out[wn], out[bn] = dw, db
+    g_next = _empty(B, S, S, p, like=g_xhat)
+    N.call("ebsdvae_conv3x3_cout1_dgrad", N.ptr(g1), N.ptr(params[wn]), N.ptr(g_next), B, S, S, p,
+           N.stream())
+    for i in reversed(range(len(plan.dec))):
+        L = plan.dec[i]
+        y, st = saved[L.name]
+        gy = in_backward(g_next, L.pmode, y, st)
+        wn, bn = L.name + ".weight", L.name + ".bias"
+        src, sst = (saved["__dec_in__"], None) if i == 0 else saved[plan.dec[i - 1].name]
+        dw = _grad_buf(grads, wn, params[wn])
+        db = _grad_buf(grads, bn, params[bn])
+        conv_wgrad(src, sst, L.src_mode, gy, L.cin, L.cout, L.kind, dw, db)
+        out[wn], out[bn] = dw, db
+        g_next = conv_dgrad(gy, L, params[wn])
+    s, C = plan.enc_side, plan.enc_channels
+    g_dec = _empty(B, s, s, C, like=g_xhat)
+    N.call("ebsdvae_upsample2_bwd", N.ptr(g_next), N.ptr(g_dec), B, s, s, C, N.stream())
+    return out, g_dec
+
+
+# ----------------------------------------------------------------------------- loss
+def loss_forward(x_hat, x, z, mu, std, kl_lambda: float):
+    """Returns (loss, kl_loss, recon_loss) 0-d tensors and per-sample (elbo, kl, recon)."""
+    B = x_hat.shape[0]
+    P = x_hat[0].numel()
+    L = z.shape[1]
+    elbo, kl, recon = _empty(B, like=x_hat), _empty(B, like=x_hat), _empty(B, like=x_hat)
+    loss, kl_loss, recon_loss = (torch.empty((), dtype=torch.float32, device=x_hat.device)
+                                 for _ in range(3))
+    N.call("ebsdvae_vae_loss_fwd", N.ptr(x_hat), N.ptr(x), N.ptr(z), N.ptr(mu), N.ptr(std),
+           float(kl_lambda), N.ptr(elbo), N.ptr(kl), N.ptr(recon), N.ptr(loss), N.ptr(kl_loss),
+           N.ptr(recon_loss), B, P, L, N.stream())
+    return (loss, kl_loss, recon_loss), (elbo, kl, recon)
+
+
+def loss_backward(x_hat, x, z, mu, std, kl_lambda: float, g_loss=None, g_kl=None, g_recon=None,
+                  g_elbo=None, scale: float = 1.0, need_gx=False, out=None):
+    """Gradients of the loss outputs w.r.t. (x_hat, z, mu, std[, x]).  `out` may supply the
+    four destination tensors (persistent buffers for graph capture)."""
+    B = x_hat.shape[0]
+    P = x_hat[0].numel()
+    L = z.shape[1]
+    if out is None:
+        out = (torch.empty_like(x_hat), torch.empty_like(z), torch.empty_like(mu),
+               torch.empty_like(std))
+    g_xhat, g_z, g_mu, g_std = out
+    g_x = torch.empty_like(x) if need_gx else None
+    N.call("ebsdvae_vae_loss_bwd", N.ptr(x_hat), N.ptr(x), N.ptr(z), N.ptr(mu), N.ptr(std),
+           float(kl_lambda), N.ptr(g_loss), N.ptr(g_kl), N.ptr(g_recon), N.ptr(g_elbo),
+           float(scale), N.ptr(g_xhat), N.ptr(g_z), N.ptr(g_mu), N.ptr(g_std), N.ptr(g_x),
+           B, P, L, N.stream())
+    return g_xhat, g_z, g_mu, g_std, g_x
+
+
+def normal_(out, seed: int, offset: int = 0, counter=None):
+    """Fill `out` with N(0,1) draws (Philox).  `counter`: optional device uint64 tensor
+    (int64 dtype) bumped on every call, for graph-replayed sampling."""
+    cptr = None
+    if counter is not None:
+        if not counter.is_cuda or counter.dtype != torch.int64:
+            raise TypeError("counter must be a device int64 tensor")
+        cptr = counter.data_ptr()
+    N.call("ebsdvae_normal_fill", N.ptr(out), out.numel(), seed & (2 ** 64 - 1),
+           offset & (2 ** 64 - 1), cptr, N.stream())
+    return out

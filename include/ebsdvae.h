@@ -1,0 +1,176 @@
+/*
+ * ebsdvae.h — C ABI of the MI355X-native VAE hot path (libebsdvae.so, gfx950).
+ *
+ * The reference (poyentung/ebsd-vae, package `latice`) has NO native boundary: its hot
+ * path is `VariationalAutoEncoderRawData.forward` (latice/model.py:40-66, built at
+ * :90-150) plus `VAELoss.compute_loss` (latice/lightning_module.py:122-156), executed as
+ * ATen ops.  Each entry point below replaces the ATen work of one of those source lines;
+ * the citation after each declaration names it.  The Python layer
+ * (ebsd-vae_amd/latice/_native.py) binds these with ctypes, exactly as INTEGRATION.md
+ * shows.
+ *
+ * Contract (every function):
+ *  - all tensor arguments are DEVICE pointers to fp32 (unless noted), NHWC for
+ *    activations; `stream` is a hipStream_t (NULL = default stream);
+ *  - the library never allocates, frees or synchronises; scratch buffers are sized with
+ *    the *_size / *_count queries and owned by the caller;
+ *  - return 0 on success; nonzero on invalid shape or launch failure, with a message in
+ *    ebsdvae_last_error() (thread-local);
+ *  - stateless: safe to call concurrently on different streams; capturable into hipGraphs.
+ *
+ * "act source" arguments (src, src_stats, src_mode) describe how a consumer reads its
+ * input: mode 0 RAW, 1 NORM = lrelu((src-mean)*rstd), 2 NORM_POOL (2x2 max of NORM, src
+ * at 2x resolution), 3 UP (nearest x2 of src at half resolution), 4 NORM_UP.
+ * src_stats is float2 {mean, rstd} per (b, c) (NULL for RAW/UP).
+ */
+#ifndef EBSDVAE_H_
+#define EBSDVAE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* ebsdvae_stream_t; /* hipStream_t */
+
+const char* ebsdvae_last_error(void);
+int ebsdvae_version(void);
+
+/* ---- weights ------------------------------------------------------------------------
+ * Pack a Conv2d (kind 0: (cout,cin,3,3), latice/model.py:95,148) or ConvTranspose2d
+ * (kind 1: (cin,cout,3,3), latice/model.py:102-104) weight into the kernel layout
+ * [tap][Cin'][Cout'].  for_dgrad=0: the forward conv (Cin'=cin, Cout'=cout);
+ * for_dgrad=1: the input-gradient conv (Cin'=cout, Cout'=cin, taps flipped). */
+int ebsdvae_pack_conv_weight(const float* src, float* dst, int cin, int cout, int kind,
+                             int for_dgrad, ebsdvae_stream_t stream);
+
+/* ---- 3x3 conv, implicit GEMM on fp32 MFMA -------------------------------------------
+ * y[b,h,w,co] = bias[co] + sum_{tap,ci} act(src)[b,h+dh,w+dw,ci] * wpack[tap][ci][co]
+ * (zero padding 1).  Replaces nn.Conv2d / nn.ConvTranspose2d forward
+ * (latice/model.py:95,102-104) and, with a for_dgrad pack and RAW source, their input
+ * gradients.  If stat_part != NULL, also writes per-tile InstanceNorm partials
+ * {mean, M2} per (b, tile, co) (count ebsdvae_conv3x3_stat_tiles per image).
+ * cin in {1} U {32k}, cout in {32, 64, 128}; W <= tile width (128x128 and 256x256 nets).
+ * bias may be NULL. */
+int ebsdvae_conv3x3_fwd(const float* src, const float* src_stats, int src_mode,
+                        const float* wpack, const float* bias, float* y, float* stat_part,
+                        int B, int H, int W, int cin, int cout, ebsdvae_stream_t stream);
+int ebsdvae_conv3x3_stat_tiles(int H, int W, int cout);
+
+/* 3x3 conv with a single output channel (the final nn.Conv2d(32,1), latice/model.py:148):
+ * out[b,h,w] = bias + sum act(src)*w[ci][tap'] with tap' = flip ? 8-tap : tap.
+ * w is (1,cin,3,3) contiguous (== (cin,1,3,3)).  With flip=1, RAW source and
+ * w = encoder.0 weight it is the input gradient of the first conv. bias may be NULL. */
+int ebsdvae_conv3x3_cout1_fwd(const float* src, const float* src_stats, int src_mode,
+                              const float* w, const float* bias, float* out, int flip,
+                              int B, int H, int W, int cin, ebsdvae_stream_t stream);
+/* input gradient of the cout=1 conv: gin[b,h,w,ci] = sum_tap g[b,h-dh,w-dw] * w[ci][tap] */
+int ebsdvae_conv3x3_cout1_dgrad(const float* g, const float* w, float* gin, int B, int H,
+                                int W, int cin, ebsdvae_stream_t stream);
+
+/* ---- weight gradients (deterministic two-level reduction) -----------------------------
+ * Partial dW[co][ci][tap] and db[co] over pixel slices; then ebsdvae_wgrad_reduce sums
+ * the slices in fixed order into the parameter-gradient layout of `kind` (0 conv,
+ * 1 convT).  Replaces autograd's convolution_backward weight/bias outputs.
+ * gy is the conv-output gradient (NHWC, cout channels); src/act as in the forward. */
+int ebsdvae_conv3x3_wgrad_slices(int B, int H, int W, int cin, int cout);
+int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, int src_mode,
+                          const float* gy, float* wpart, float* bpart, int B, int H, int W,
+                          int cin, int cout, ebsdvae_stream_t stream);
+int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
+                         float* db, int cin, int cout, int kind, ebsdvae_stream_t stream);
+
+/* ---- InstanceNorm2d + LeakyReLU (latice/model.py:96-97,105-106) -----------------------
+ * combine conv-epilogue partials {mean,M2} (tiles per image, n elements each) into
+ * {mean, rstd} per (b,c). */
+int ebsdvae_in_stats_finalize(const float* part, float* stats, int B, int C, int tiles,
+                              int n_per_tile, ebsdvae_stream_t stream);
+/* materialise act(src) at logical (B,H,W,C) NHWC (e.g. the encoder output after the last
+ * MaxPool2d, latice/model.py:124) */
+int ebsdvae_act_apply(const float* src, const float* src_stats, int src_mode, float* out,
+                      int B, int H, int W, int C, ebsdvae_stream_t stream);
+/* backward through [pool|upsample] . LeakyReLU . InstanceNorm of one block.
+ * gnext: gradient w.r.t. the consumer's input; pmode 0 identity, 1 the consumer pooled
+ * (gnext at H/2), 2 the consumer upsampled (gnext at 2H).  y/stats: the block's saved
+ * pre-norm output and statistics.  Two passes: reduce -> bstats {mean(g_xhat),
+ * mean(g_xhat*xhat)} per (b,c), then apply -> gy (conv-output gradient, (B,H,W,C)). */
+int ebsdvae_in_bwd_tiles(int H, int W, int C);
+int ebsdvae_in_bwd_reduce(const float* gnext, int pmode, const float* y, const float* stats,
+                          float* part, int B, int H, int W, int C, ebsdvae_stream_t stream);
+int ebsdvae_in_bwd_finalize(const float* part, float* bstats, int B, int C, int tiles,
+                            int HW, ebsdvae_stream_t stream);
+int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* y, const float* stats,
+                         const float* bstats, float* gy, int B, int H, int W, int C,
+                         ebsdvae_stream_t stream);
+/* gradient of nearest x2 upsampling: out[b,h,w,c] = sum of the 2x2 block of g (at 2H) */
+int ebsdvae_upsample2_bwd(const float* g, float* out, int B, int H, int W, int C,
+                          ebsdvae_stream_t stream);
+
+/* ---- latent heads + reparameterisation (latice/model.py:55-64, 25-38) ----------------
+ * enc: encoder output (B,S,S,C) NHWC.  flat = enc in NCHW flatten order (saved for
+ * backward); mu/logvar = Linear(F,L); std = exp(logvar/2); z = mu + eps*std;
+ * dec_in = Linear(L,F)(z) viewed (B,C,S,S) and written NHWC. */
+int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const float* b_mu,
+                      const float* w_lv, const float* b_lv, const float* w_l2,
+                      const float* b_l2, const float* eps, float* flat, float* mu,
+                      float* std, float* z, float* dec_in, int B, int C, int S, int L,
+                      ebsdvae_stream_t stream);
+/* g_dec: grad of dec_in (B,S,S,C NHWC); g_z/g_mu/g_std: direct output grads (may be
+ * NULL = 0).  Writes g_enc (B,S,S,C NHWC) and per-sample scratch
+ * gs = [g_mu_tot (B,L) | g_logvar (B,L) | g_out (B,F)] consumed by heads_wgrad. */
+int ebsdvae_heads_bwd(const float* g_dec, const float* g_z, const float* g_mu,
+                      const float* g_std, const float* std, const float* eps,
+                      const float* w_mu, const float* w_lv, const float* w_l2, float* g_enc,
+                      float* gs, int B, int C, int S, int L, ebsdvae_stream_t stream);
+int ebsdvae_heads_wgrad(const float* flat, const float* z, const float* gs, float* gw_mu,
+                        float* gb_mu, float* gw_lv, float* gb_lv, float* gw_l2,
+                        float* gb_l2, int B, int F, int L, ebsdvae_stream_t stream);
+
+/* generic Linear (y = x W^T + b), for direct calls of model.mu / .logvar / .linear2 */
+int ebsdvae_linear_fwd(const float* x, const float* w, const float* b, float* y, int M,
+                       int K, int N, ebsdvae_stream_t stream);
+int ebsdvae_linear_bwd(const float* x, const float* w, const float* gy, float* gx,
+                       float* gw, float* gb, int M, int K, int N, ebsdvae_stream_t stream);
+/* VariationalAutoEncoder.reparameterize (latice/model.py:25-38) */
+int ebsdvae_reparam_fwd(const float* mu, const float* logvar, const float* eps, float* z,
+                        float* std, int64_t n, ebsdvae_stream_t stream);
+int ebsdvae_reparam_bwd(const float* gz, const float* gstd, const float* eps,
+                        const float* std, float* gmu, float* glogvar, int64_t n,
+                        ebsdvae_stream_t stream);
+/* standard-normal sampler (counter-based Philox4x32-10 + Box-Muller) for eps
+ * (replaces torch.distributions.Normal.rsample's normal_, latice/model.py:36-37).
+ * If counter != NULL (device uint64), it is incremented first and the draw uses
+ * offset + counter * ceil(n/4) as its Philox counter base, so a captured graph draws
+ * fresh noise on every replay. */
+int ebsdvae_normal_fill(float* out, int64_t n, uint64_t seed, uint64_t offset,
+                        uint64_t* counter, ebsdvae_stream_t stream);
+
+/* ---- loss (latice/lightning_module.py:79-156) ----------------------------------------
+ * recon_b = mean_p BCEWithLogits(x_hat, x); kl_b = kl_lambda * mean_j [0.5 z^2 -
+ * 0.5 ((z-mu)/std)^2 - log std]; elbo_b = kl_b + recon_b;
+ * loss = mean elbo, kl_loss = mean kl, recon_loss = mean recon (device scalars). */
+int ebsdvae_vae_loss_fwd(const float* x_hat, const float* x, const float* z, const float* mu,
+                         const float* std, float kl_lambda, float* elbo, float* kl,
+                         float* recon, float* loss, float* kl_loss, float* recon_loss, int B,
+                         int P, int L, ebsdvae_stream_t stream);
+/* upstream gradients g_loss, g_kl_loss, g_recon_loss (device scalars) and g_elbo (B) may
+ * each be NULL (= 0); scale multiplies all of them (e.g. 1/world_size for data
+ * parallelism).  g_x (gradient w.r.t. the BCE target) may be NULL. */
+int ebsdvae_vae_loss_bwd(const float* x_hat, const float* x, const float* z, const float* mu,
+                         const float* std, float kl_lambda, const float* g_loss,
+                         const float* g_kl_loss, const float* g_recon_loss,
+                         const float* g_elbo, float scale, float* g_xhat, float* g_z,
+                         float* g_mu, float* g_std, float* g_x, int B, int P, int L,
+                         ebsdvae_stream_t stream);
+
+/* ---- optimiser (torch.optim.Adam semantics; latice/lightning_module.py:26-28) ---------
+ * state: device float step counter (incremented by this call), m, v, vmax (amsgrad). */
+int ebsdvae_adam(float* p, const float* g, float* m, float* v, float* vmax, float* step,
+                 int64_t n, float lr, float beta1, float beta2, float eps,
+                 float weight_decay, int amsgrad, ebsdvae_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EBSDVAE_H_ */

@@ -1,0 +1,291 @@
+"""Kernel-level parity: every HIP entry point vs the numpy oracle primitives (float64),
+seeded random inputs at sizes the oracle finishes in seconds.  Tolerances are norm-wise
+(max|d| / max|ref|) and stated per test."""
+import numpy as np
+import pytest
+import torch
+
+from latice import _native as N
+from latice import engine as E
+from oracle import vae_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5   # fp32 single-layer ops vs float64
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy().astype(np.float64)
+
+
+def act_oracle(src, mean, rstd, mode):
+    """Logical conv input from a source tensor under an act mode (NHWC float64)."""
+    if mode == E.ACT_RAW:
+        return src
+    if mode == E.ACT_UP:
+        return O.upsample2(src)
+    a = O.lrelu((src - mean) * rstd)
+    if mode == E.ACT_NORM:
+        return a
+    if mode == E.ACT_NORM_POOL:
+        return O.maxpool2(a)[0]
+    return O.upsample2(a)
+
+
+def src_shape(B, H, C, mode):
+    if mode == E.ACT_NORM_POOL:
+        return (B, 2 * H, 2 * H, C)
+    if mode in (E.ACT_UP, E.ACT_NORM_UP):
+        return (B, H // 2, H // 2, C)
+    return (B, H, H, C)
+
+
+def make_src(rng, B, H, C, mode):
+    s = rng.standard_normal(src_shape(B, H, C, mode)) * 1.5 + 0.3
+    mean = s.mean(axis=(1, 2), keepdims=True)
+    rstd = 1.0 / np.sqrt(s.var(axis=(1, 2), keepdims=True) + 1e-5)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)   # (B, C, 2)
+    return s, mean, rstd, st
+
+
+# (cin, cout, H, mode) covering every conv configuration of the 128 and 256 networks
+FWD_CASES = [
+    (1, 32, 128, E.ACT_RAW), (32, 32, 128, E.ACT_NORM), (32, 64, 64, E.ACT_NORM_POOL),
+    (64, 64, 64, E.ACT_NORM), (64, 128, 32, E.ACT_NORM_POOL), (128, 128, 16, E.ACT_NORM_POOL),
+    (128, 128, 8, E.ACT_NORM_POOL), (128, 128, 8, E.ACT_UP), (128, 128, 16, E.ACT_NORM_UP),
+    (128, 64, 32, E.ACT_NORM), (64, 32, 64, E.ACT_NORM), (32, 32, 128, E.ACT_NORM_UP),
+    (32, 32, 256, E.ACT_NORM), (64, 32, 64, E.ACT_RAW), (128, 64, 32, E.ACT_RAW),
+    (64, 128, 32, E.ACT_RAW), (32, 64, 64, E.ACT_RAW),
+]
+
+
+@pytest.mark.parametrize("cin,cout,H,mode", FWD_CASES)
+def test_conv3x3_fwd_and_in_stats(cuda, cin, cout, H, mode):
+    rng = np.random.default_rng(cin * 1000 + cout + H + mode)
+    B = 3 if H <= 64 else 2
+    s, mean, rstd, st = make_src(rng, B, H, cin, mode)
+    w = rng.standard_normal((cout, cin, 3, 3)) / np.sqrt(9 * cin)
+    b = rng.standard_normal(cout) * 0.1
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
+    y, stt = E.conv_forward(dev(s), dev(st) if mode in (1, 2, 4) else None, layer, dev(w), dev(b), B)
+    ref = O.conv3x3(act_oracle(s, mean, rstd, mode), w, b)
+    assert O.rel_err(host(y), ref) < TOL
+    _, rm, rr = O.instance_norm(ref)
+    got = host(stt)
+    assert O.rel_err(got[..., 0], rm[:, 0, 0, :]) < 1e-5
+    assert O.rel_err(got[..., 1], rr[:, 0, 0, :]) < 1e-4
+
+
+@pytest.mark.parametrize("kind", [E.KIND_CONV, E.KIND_CONVT])
+@pytest.mark.parametrize("cin,cout,H", [(32, 64, 32), (128, 128, 8), (64, 32, 64), (128, 64, 16)])
+def test_conv_dgrad_matches_oracle(cuda, kind, cin, cout, H):
+    rng = np.random.default_rng(7 + cin + cout + H + kind)
+    B = 2
+    gy = rng.standard_normal((B, H, H, cout))
+    wsrc = rng.standard_normal((cout, cin, 3, 3) if kind == 0 else (cin, cout, 3, 3)) * 0.1
+    wc = wsrc if kind == 0 else O.conv_w_from_convT(wsrc)
+    layer = E.ConvLayer("t", kind, cin, cout, H, E.ACT_RAW, 0)
+    gin = E.conv_dgrad(dev(gy), layer, dev(wsrc))
+    assert O.rel_err(host(gin), O.conv3x3_dgrad(gy, wc)) < TOL
+
+
+WG_CASES = [
+    (1, 32, 128, E.ACT_RAW, 0), (32, 32, 128, E.ACT_NORM, 0), (32, 64, 64, E.ACT_NORM_POOL, 0),
+    (64, 128, 32, E.ACT_NORM_POOL, 0), (128, 128, 8, E.ACT_NORM_POOL, 0),
+    (128, 128, 8, E.ACT_UP, 1), (128, 64, 32, E.ACT_NORM, 1), (64, 32, 64, E.ACT_NORM, 1),
+    (32, 32, 128, E.ACT_NORM_UP, 1), (32, 1, 128, E.ACT_NORM, 0),
+]
+
+
+@pytest.mark.parametrize("cin,cout,H,mode,kind", WG_CASES)
+def test_conv_wgrad_matches_oracle(cuda, cin, cout, H, mode, kind):
+    rng = np.random.default_rng(11 + cin + cout + H + mode)
+    B = 3 if H <= 64 else 2
+    s, mean, rstd, st = make_src(rng, B, H, cin, mode)
+    gshape = (B, H, H) if cout == 1 else (B, H, H, cout)
+    gy = rng.standard_normal(gshape)
+    wshape = (cout, cin, 3, 3) if kind == 0 else (cin, cout, 3, 3)
+    dw = torch.empty(wshape, device="cuda")
+    db = torch.empty(cout, device="cuda")
+    E.conv_wgrad(dev(s), dev(st) if mode in (1, 2, 4) else None, mode, dev(gy), cin, cout, kind, dw, db)
+    a = act_oracle(s, mean, rstd, mode)
+    rw, rb = O.conv3x3_wgrad(a, gy.reshape(B, H, H, cout))
+    if kind == 1:
+        rw = rw.transpose(1, 0, 2, 3)[:, :, ::-1, ::-1]
+    assert O.rel_err(host(dw), rw) < 5e-5
+    assert O.rel_err(host(db), rb) < 5e-5
+
+
+@pytest.mark.parametrize("pmode,H,C", [(E.P_ID, 64, 32), (E.P_POOL, 32, 64), (E.P_POOL, 8, 128),
+                                       (E.P_UP, 16, 128), (E.P_UP, 64, 32), (E.P_ID, 128, 32)])
+def test_instance_norm_backward(cuda, pmode, H, C):
+    rng = np.random.default_rng(3 + pmode + H + C)
+    B = 2
+    y = rng.standard_normal((B, H, H, C)) * 2 + 0.5
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    gshape = {E.P_ID: (B, H, H, C), E.P_POOL: (B, H // 2, H // 2, C), E.P_UP: (B, 2 * H, 2 * H, C)}[pmode]
+    gn = rng.standard_normal(gshape)
+    gy = E.in_backward(dev(gn), pmode, dev(y), dev(st))
+    a = O.lrelu(xh)
+    if pmode == E.P_POOL:
+        _, arg = O.maxpool2(a)
+        ga = O.maxpool2_bwd(gn, arg)
+    elif pmode == E.P_UP:
+        ga = O.upsample2_bwd(gn)
+    else:
+        ga = gn
+    ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
+    assert O.rel_err(host(gy), ref) < 1e-4
+
+
+def test_act_apply_and_upsample_bwd(cuda):
+    rng = np.random.default_rng(5)
+    s, mean, rstd, st = make_src(rng, 3, 4, 128, E.ACT_NORM_POOL)
+    out = torch.empty(3, 4, 4, 128, device="cuda")
+    ds, dst = dev(s), dev(st)     # keep the inputs alive until the kernel has run
+    N.call("ebsdvae_act_apply", N.ptr(ds), N.ptr(dst), E.ACT_NORM_POOL, N.ptr(out), 3, 4, 4,
+           128, N.stream())
+    assert O.rel_err(host(out), act_oracle(s, mean, rstd, E.ACT_NORM_POOL)) < 1e-5
+    g = rng.standard_normal((3, 8, 8, 128))
+    o2 = torch.empty(3, 4, 4, 128, device="cuda")
+    dg = dev(g)
+    N.call("ebsdvae_upsample2_bwd", N.ptr(dg), N.ptr(o2), 3, 4, 4, 128, N.stream())
+    assert O.rel_err(host(o2), O.upsample2_bwd(g)) < 1e-6
+
+
+def test_cout1_conv_fwd_dgrad_and_first_conv_input_grad(cuda):
+    rng = np.random.default_rng(9)
+    B, H = 2, 128
+    s, mean, rstd, st = make_src(rng, B, H, 32, E.ACT_NORM)
+    w = rng.standard_normal((1, 32, 3, 3)) * 0.1
+    b = np.array([0.3])
+    out = torch.empty(B, 1, H, H, device="cuda")
+    ds, dst, dw, db = dev(s), dev(st), dev(w), dev(b)
+    N.call("ebsdvae_conv3x3_cout1_fwd", N.ptr(ds), N.ptr(dst), E.ACT_NORM, N.ptr(dw),
+           N.ptr(db), N.ptr(out), 0, B, H, H, 32, N.stream())
+    a = act_oracle(s, mean, rstd, E.ACT_NORM)
+    assert O.rel_err(host(out)[:, 0], O.conv3x3(a, w, b)[..., 0]) < TOL
+    g = rng.standard_normal((B, H, H))
+    gin = torch.empty(B, H, H, 32, device="cuda")
+    dg = dev(g)
+    N.call("ebsdvae_conv3x3_cout1_dgrad", N.ptr(dg), N.ptr(dw), N.ptr(gin), B, H, H, 32,
+           N.stream())
+    assert O.rel_err(host(gin), O.conv3x3_dgrad(g[..., None], w)) < TOL
+    # input gradient of the first conv (1 -> 32) = flipped cout1 conv over gy
+    w0 = rng.standard_normal((32, 1, 3, 3)) * 0.2
+    gy = rng.standard_normal((B, H, H, 32))
+    gx = torch.empty(B, 1, H, H, device="cuda")
+    dgy, dw0 = dev(gy), dev(w0)
+    N.call("ebsdvae_conv3x3_cout1_fwd", N.ptr(dgy), None, E.ACT_RAW, N.ptr(dw0), None,
+           N.ptr(gx), 1, B, H, H, 32, N.stream())
+    assert O.rel_err(host(gx)[:, 0], O.conv3x3_dgrad(gy, w0)[..., 0]) < TOL
+
+
+@pytest.mark.parametrize("S,L", [(128, 16), (256, 64)])
+def test_heads_forward_backward(cuda, S, L):
+    rng = np.random.default_rng(S + L)
+    plan = E.build_plan(32, L, S)
+    B, s, C, F = 5, plan.enc_side, plan.enc_channels, plan.feat
+    enc = rng.standard_normal((B, s, s, C))
+    p = {"mu.0.weight": rng.standard_normal((L, F)) * 0.02, "mu.0.bias": rng.standard_normal(L) * 0.1,
+         "logvar.0.weight": rng.standard_normal((L, F)) * 0.02,
+         "logvar.0.bias": rng.standard_normal(L) * 0.1,
+         "linear2.0.weight": rng.standard_normal((F, L)) * 0.2,
+         "linear2.0.bias": rng.standard_normal(F) * 0.1}
+    eps = rng.standard_normal((B, L))
+    pd = {k: dev(v) for k, v in p.items()}
+    flat, mu, std, z, dec_in = E.heads_forward(plan, dev(enc), pd, dev(eps))
+    rflat = O.nchw_flatten(enc)
+    rmu = rflat @ p["mu.0.weight"].T + p["mu.0.bias"]
+    rlv = rflat @ p["logvar.0.weight"].T + p["logvar.0.bias"]
+    rstd = np.exp(rlv / 2)
+    rz = rmu + eps * rstd
+    rout = rz @ p["linear2.0.weight"].T + p["linear2.0.bias"]
+    assert O.rel_err(host(flat), rflat) < 1e-7
+    for got, ref in ((mu, rmu), (std, rstd), (z, rz)):
+        assert O.rel_err(host(got), ref) < 1e-5
+    assert O.rel_err(host(dec_in), O.nchw_unflatten(rout, C, s)) < 1e-5
+    # backward
+    g_dec = rng.standard_normal((B, s, s, C))
+    gz, gmu, gstd = (rng.standard_normal((B, L)) for _ in range(3))
+    g_enc, grads = E.heads_backward(plan, dev(g_dec), dev(gz), dev(gmu), dev(gstd), flat, std, z,
+                                    dev(eps), pd)
+    g_out = O.nchw_flatten(g_dec)
+    gzt = g_out @ p["linear2.0.weight"] + gz
+    gmt = gzt + gmu
+    glv = (gstd + gzt * eps) * rstd / 2
+    ref = {"linear2.0.weight": g_out.T @ rz, "linear2.0.bias": g_out.sum(0),
+           "mu.0.weight": gmt.T @ rflat, "mu.0.bias": gmt.sum(0),
+           "logvar.0.weight": glv.T @ rflat, "logvar.0.bias": glv.sum(0)}
+    for k, v in ref.items():
+        assert O.rel_err(host(grads[k]), v) < 1e-4, k
+    rgenc = O.nchw_unflatten(gmt @ p["mu.0.weight"] + glv @ p["logvar.0.weight"], C, s)
+    assert O.rel_err(host(g_enc), rgenc) < 1e-4
+
+
+@pytest.mark.parametrize("B,P", [(4, 128 * 128), (3, 250)])
+def test_vae_loss_forward_backward(cuda, B, P):
+    rng = np.random.default_rng(B + P)
+    L = 16
+    xh = rng.standard_normal((B, P)) * 3
+    x = np.floor(rng.random((B, P)) * 255) / 255
+    mu = rng.standard_normal((B, L))
+    std = np.exp(rng.standard_normal((B, L)) * 0.3)
+    z = mu + rng.standard_normal((B, L)) * std
+    lam = 0.1
+    t = [dev(a) for a in (xh, x, z, mu, std)]
+    (loss, kl_loss, rec_loss), (elbo, kl, rec) = E.loss_forward(*t, lam)
+    ref = O.vae_loss(xh.reshape(B, 1, 1, P), x.reshape(B, 1, 1, P), z, mu, std, lam)
+    assert abs(float(loss) - ref["loss"]) < 1e-6 * max(1, abs(ref["loss"]))
+    assert abs(float(kl_loss) - ref["kl_loss"]) < 1e-5 * max(1e-3, abs(ref["kl_loss"]))
+    assert O.rel_err(host(elbo), ref["elbo"]) < 1e-6
+    one = torch.ones((), device="cuda")
+    g_xhat, g_z, g_mu, g_std, g_x = E.loss_backward(*t, lam, g_loss=one, need_gx=True)
+    sig = 1 / (1 + np.exp(-xh))
+    assert O.rel_err(host(g_xhat), (sig - x) / (P * B)) < 1e-5
+    assert O.rel_err(host(g_x), -xh / (P * B)) < 1e-5
+    c = lam / (B * L)
+    assert O.rel_err(host(g_z), c * (z - (z - mu) / std ** 2)) < 1e-5
+    assert O.rel_err(host(g_mu), c * (z - mu) / std ** 2) < 1e-5
+    assert O.rel_err(host(g_std), c * ((z - mu) ** 2 / std ** 3 - 1 / std)) < 1e-5
+
+
+def test_normal_sampler(cuda):
+    a = torch.empty(1 << 20, device="cuda")
+    b = torch.empty(1 << 20, device="cuda")
+    E.normal_(a, 1234)
+    E.normal_(b, 1234)
+    assert torch.equal(a, b)
+    m, s = float(a.mean()), float(a.std())
+    assert abs(m) < 5e-3 and abs(s - 1) < 5e-3
+    E.normal_(b, 1235)
+    assert not torch.equal(a, b)
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    E.normal_(a, 7, counter=ctr)
+    E.normal_(b, 7, counter=ctr)
+    assert int(ctr) == 2 and not torch.equal(a, b)
+
+
+@pytest.mark.parametrize("amsgrad", [False, True])
+def test_fused_adam_matches_torch_adam(cuda, amsgrad):
+    from latice.optim import FusedAdam
+    torch.manual_seed(0)
+    p0 = torch.randn(10007, device="cuda")
+    pa = p0.clone().requires_grad_(True)
+    pb = p0.clone().requires_grad_(True)
+    oa = FusedAdam([pa], lr=1e-3, amsgrad=amsgrad, weight_decay=0.01)
+    ob = torch.optim.Adam([pb], lr=1e-3, amsgrad=amsgrad, weight_decay=0.01, foreach=False)
+    for _ in range(5):
+        g = torch.randn(10007, device="cuda")
+        pa.grad = g.clone()
+        pb.grad = g.clone()
+        oa.step()
+        ob.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(pa, pb, rtol=1e-6, atol=1e-7)

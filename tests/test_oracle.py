@@ -1,0 +1,67 @@
+"""The oracle (oracle/vae_oracle.py) pinned against golden vectors produced by the
+reference itself (tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from latice.seeding import layer_table, seeded_state_dict
+from oracle import vae_oracle as O
+
+FIXTURES = ["vae128_b4", "vae128_b8_c1", "vae128_b2_edge", "vae256_b2_l64"]
+
+
+def _case(name):
+    f = O.load_fixture(os.path.join(GOLDEN, name + ".npz"))
+    B, S, L, ws, xs = (int(v) for v in f["meta"])
+    sd = seeded_state_dict(ws, 32, L, S)
+    return f, sd
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_oracle_forward_matches_reference(name):
+    f, sd = _case(name)
+    outs, _ = O.forward(sd, f["x"], f["eps"])
+    for k in ("mu", "std", "z"):
+        assert O.rel_err(outs[k], f[k]) < 1e-10, k
+    if "x_hat" in f:
+        assert O.rel_err(outs["x_hat"], f["x_hat"]) < 1e-6
+    else:
+        assert O.rel_err(outs["x_hat"].ravel()[f["x_hat_idx"]], f["x_hat_sub"]) < 1e-6
+    assert O.rel_err(outs["enc_out"], f["enc_out"]) < 1e-6
+    ls = O.vae_loss(outs["x_hat"], f["x"], outs["z"], outs["mu"], outs["std"], float(f["kl_lambda"]))
+    for k in ("loss", "kl_loss", "recon_loss"):
+        assert abs(ls[k] - float(f[k])) <= 1e-12 + 1e-10 * abs(float(f[k])), k
+    assert O.rel_err(ls["elbo"], f["elbo"]) < 1e-10
+
+
+@pytest.mark.parametrize("name", ["vae128_b4", "vae256_b2_l64"])
+def test_oracle_backward_matches_reference_autograd(name):
+    """The hand-derived backward (IN/LReLU/pool/upsample/heads/KL adjoints) equals torch
+    autograd through the reference model."""
+    f, sd = _case(name)
+    outs, cache = O.forward(sd, f["x"], f["eps"])
+    g = O.backward(cache, f["x"], float(f["kl_lambda"]))
+    for n in f["grad_names"]:
+        ref = f["grad_full/" + n] if "grad_full/" + n in f else f["grad_sub/" + n]
+        got = g[n] if "grad_full/" + n in f else g[n].ravel()[f["grad_idx/" + n]]
+        if n.endswith(".bias") and not n.startswith(("mu", "logvar", "linear2", "decoder.14")):
+            # analytically zero (conv bias feeding an affine-free InstanceNorm)
+            assert np.abs(got).max() < 1e-9 and np.abs(ref).max() < 1e-9, n
+        else:
+            assert O.rel_err(got, ref) < 1e-6, n
+
+
+def test_golden_param_order_matches_seeding_table():
+    f, _ = _case("vae128_b4")
+    names = [r[0] for r in layer_table()]
+    assert list(f["grad_names"]) == names
+    assert len(names) == 46
+
+
+def test_fixture_inputs_are_quantised():
+    f, _ = _case("vae128_b8_c1")
+    x = f["x"]
+    assert x.dtype == np.float32 and x.min() >= 0 and x.max() <= 1
+    assert np.allclose(x * 255.0, np.round(x * 255.0), atol=1e-4)
