@@ -1,0 +1,197 @@
+"""Benchmark: EBSD VAE training step on MI355X (BASELINE.json config c2/c3).
+
+One "step" = forward (encoder -> reparameterise -> decoder) + BCE/KL loss + backward +
+(N>1: RCCL gradient all-reduce) + Adam, on B synthetic 128x128 fp32 patterns per GPU
+(weak scaling), seeded kaiming-uniform weights of the reference architecture.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256]
+    torchrun --nproc-per-node N ... bench.py --gpus N ...     (N > 1, one rank per GPU)
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus:
+  roofline      the dominant kernel family (by GPU time), its algorithmic FLOPs per
+                launch / average launch duration (HIP events on the launch stream, live in
+                the timed region) against the fp32 MFMA peak (157.3 TFLOP/s);
+  cpu_baseline  oracle/torch_port.py (PyTorch-CPU restatement of the reference
+                training_step) timed on this host's cores on a bounded sample (N=1, rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "ebsd-vae_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3      # MI355X fp32 MFMA (= fp32 vector) dense peak
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def step_flops_per_pattern(plan) -> float:
+    """Algorithmic FLOPs of one pattern through fwd + bwd (convs + linears)."""
+    from latice.engine import conv_flops
+    f = 0.0
+    for i, L in enumerate(plan.enc + plan.dec):
+        c = conv_flops(1, L.H, L.H, L.cin, L.cout)
+        f += c * (2 if (i == 0) else 3)          # fwd + wgrad (+ dgrad except the first conv)
+    S = plan.image_size
+    f += 3 * conv_flops(1, S, S, plan.inplanes, 1)  # final conv fwd + dgrad + wgrad
+    lin = 2 * plan.feat * plan.latent_dim * 3       # mu, logvar, linear2
+    return f + 3 * lin
+
+
+def cpu_baseline(plan, seconds: float, batch: int):
+    from latice.seeding import seeded_state_dict, synthetic_patterns
+    from oracle.torch_port import CPUStep   # oracle: the baseline leg only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    sd = seeded_state_dict(0, plan.inplanes, plan.latent_dim, plan.image_size)
+    st = CPUStep(sd, kl_lambda=5e-6)
+    x = torch.from_numpy(synthetic_patterns(123, batch, plan.image_size))
+    eps = torch.randn(batch, plan.latent_dim)
+    st.step(x, eps)                     # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        st.step(x, eps)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(n * batch / el, 3), "unit": "patterns/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} timed steps (+1 warm-up) of fwd+loss+bwd+Adam at batch {batch}, "
+                      f"{plan.image_size}x{plan.image_size}, PyTorch-CPU restatement "
+                      f"(oracle/torch_port.py), {threads} threads, {cpu}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="patterns per GPU")
+    ap.add_argument("--image-size", type=int, default=128)
+    ap.add_argument("--latent-dim", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-batch", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+
+    from latice import engine as E
+    from latice.model import VariationalAutoEncoderRawData
+    from latice.seeding import seeded_state_dict, synthetic_patterns
+    from latice.trainer import VAETrainer
+
+    model = VariationalAutoEncoderRawData(32, args.latent_dim, args.image_size)
+    sd = seeded_state_dict(0, 32, args.latent_dim, args.image_size)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model = model.to(dev)
+    trainer = VAETrainer(model, kl_lambda=5e-6, lr=1e-4, seed=1000 + rank)
+    x = torch.from_numpy(synthetic_patterns(rank, args.batch, args.image_size)).to(dev)
+    plan = model.plan
+
+    log(f"[bench] rank {rank}/{world} batch {args.batch} warmup {args.warmup} steps {args.steps}")
+    for _ in range(args.warmup):
+        trainer.step(x)
+    torch.cuda.synchronize()
+
+    probe = E.probe() if not args.no_probe else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if probe is not None:
+        with probe:
+            for _ in range(args.steps):
+                out = trainer.step(x)
+    else:
+        for _ in range(args.steps):
+            out = trainer.step(x)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    loss = float(out[0])
+    ms = elapsed / args.steps * 1e3
+    value = world * args.batch * args.steps / elapsed
+
+    roof = None
+    fam = {}
+    if probe is not None:
+        fam = probe.summary()
+        dom = max(fam, key=lambda k: fam[k]["ms"])
+        d = fam[dom]
+        flops_per_launch = d["flops"] / d["launches"]
+        avg_s = d["ms"] / d["launches"] / 1e3
+        ach = flops_per_launch / avg_s / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
+                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "launches_per_step": d["launches"] // args.steps,
+                "avg_launch_us": round(avg_s * 1e6, 2),
+                "gflop_per_launch": round(flops_per_launch / 1e9, 3)}
+    step_tflops = step_flops_per_pattern(plan) * args.batch / (ms / 1e3) / 1e12
+
+    res = {
+        "metric": "EBSD patterns/sec (128x128, fwd+bwd)" if args.image_size == 128
+        else f"EBSD patterns/sec ({args.image_size}x{args.image_size}, fwd+bwd)",
+        "value": round(value, 2), "unit": "patterns/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": f"c{2 if world == 1 else 3}: VariationalAutoEncoderRawData "
+                               f"{args.image_size}x{args.image_size}, latent {args.latent_dim}, "
+                               f"batch {args.batch}/GPU, fwd+loss+bwd+Adam"
+                               + (" + RCCL grad all-reduce" if world > 1 else ""),
+                   "global_batch": world * args.batch, "image_size": args.image_size,
+                   "latent_dim": args.latent_dim, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "step_fp32_tflops": round(step_tflops, 2),
+        "step_frac_of_fp32_peak": round(step_tflops / FP32_PEAK_TFLOPS, 4),
+        "loss": round(loss, 6),
+        "kernel_families_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in fam.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("[bench] cpu baseline ...")
+        res["cpu_baseline"] = cpu_baseline(plan, args.cpu_seconds, args.cpu_batch)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -273,7 +273,11 @@ static int launch_fwd(const FwdCfg& c, const float* src, const float* st, int mo
                       const float* wp, const float* bias, float* y, float* part, int B, int H,
                       int W, int cin, hipStream_t s) {
   auto k = conv3x3_fwd_kernel<WM, MF, NF, CIN1>;
-  if (c.lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
+  static bool attr_done = false;   // once per instantiation (keeps graph capture clean)
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_done = true;
+  }
   const int blocks = (c.NI > 1) ? (B + c.NI - 1) / c.NI : B * (H / c.TH);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), c.lds, s, src, (const float2*)st, mode, wp, bias,
                      y, (float2*)part, B, H, W, cin, c.TH, c.NI);

@@ -64,19 +64,20 @@ EV_DEVINL void tile_origin(int t, const WgGeom& g, int& b0, int& y0, int& x0) {
 }
 
 // ------------------------------------------------------------------ generic (cin % 32 == 0)
-template <int NWCO>
-__global__ __launch_bounds__(NWCO * 128) void wgrad_kernel(
+template <int NWCO, int KSPLIT>
+__global__ __launch_bounds__(256) void wgrad_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, int smode,
     const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
     int H, int W, int Cin, int Cout, WgGeom g) {
   constexpr int CO_T = NWCO * 32;
   constexpr int GS = CO_T + 16;
-  constexpr int NT = NWCO * 128;
+  constexpr int NT = 256;
+  static_assert(NWCO * 2 * KSPLIT == 4, "4 waves per block");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lg = smem;                 // [128][GS]
   float* la = smem + WG_PT * GS;    // [halo px][48]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wco = wave % NWCO, wci = wave / NWCO;
+  const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
   const int slice = blockIdx.x, co0 = blockIdx.y * CO_T, ci0 = blockIdx.z * 32;
   const int HP = g.TH + 2, WP = g.TW + 2, halo = g.NI * HP * WP;
   const int l16 = lane & 15, kq = lane >> 4;
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(NWCO * 128) void wgrad_kernel(
   for (int f = 0; f < 2; ++f)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;   // bias partial for co0 + tid (tid < CO_T), ci tile 0 only
+  double bsum = 0.0;  // bias partial for co0 + tid (tid < CO_T), ci tile 0 only
 
   const int t_beg = slice * g.tps;
   const int t_end = min(t_beg + g.tps, g.tiles);
@@ -118,10 +119,12 @@ __global__ __launch_bounds__(NWCO * 128) void wgrad_kernel(
     }
     __syncthreads();
     if (blockIdx.z == 0 && tid < CO_T) {
-      for (int px = 0; px < WG_PT; ++px) bsum += lg[px * GS + tid];
+      float ts = 0.f;
+      for (int px = 0; px < WG_PT; ++px) ts += lg[px * GS + tid];
+      bsum += (double)ts;
     }
 #pragma unroll 2
-    for (int s = 0; s < WG_PT / 4; ++s) {
+    for (int s = wk; s < WG_PT / 4; s += KSPLIT) {
       const int px = 4 * s + kq;
       const int img = px / tpx, rem = px - img * tpx;
       const int r = rem / g.TW, c = rem - r * g.TW;
@@ -137,18 +140,42 @@ __global__ __launch_bounds__(NWCO * 128) void wgrad_kernel(
       }
     }
   }
+  if (KSPLIT == 2) {   // fold the second K half into the first through LDS
+    __syncthreads();
+    float* xs = smem + (size_t)(wave - 2 * NWCO) * 72 * 64;
+    if (wk == 1) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xs[((f * 9 + tap) * 4 + r) * 64 + lane] = acc[f][tap][r];
+    }
+    __syncthreads();
+    if (wk == 0) {
+      xs = smem + (size_t)wave * 72 * 64;
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[f][tap][r] += xs[((f * 9 + tap) * 4 + r) * 64 + lane];
+    }
+  }
   // partial layout [slice][tap][co][ci]
   const int ci = ci0 + wci * 16 + l16;
+  if (wk == 0) {
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
+    for (int f = 0; f < 2; ++f)
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
+      for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco * 32 + f * 16 + kq * 4 + r;
-        wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] = acc[f][tap][r];
-      }
-  if (blockIdx.z == 0 && tid < CO_T) bpart[(size_t)slice * Cout + co0 + tid] = bsum;
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wco * 32 + f * 16 + kq * 4 + r;
+          wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] = acc[f][tap][r];
+        }
+  }
+  if (blockIdx.z == 0 && tid < CO_T) bpart[(size_t)slice * Cout + co0 + tid] = (float)bsum;
 }
 
 // ------------------------------------------------------------------ cin == 1 (first conv)
@@ -168,7 +195,7 @@ __global__ __launch_bounds__(128) void wgrad_cin1_kernel(
   const int tapj = l16 < 9 ? l16 : 0;
   const int tkh = tapj / 3, tkw = tapj % 3;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
+  double bsum = 0.0;
   const int t_beg = slice * g.tps, t_end = min(t_beg + g.tps, g.tiles);
   const int tpx = g.TH * g.TW;
   for (int t = t_beg; t < t_end; ++t) {
@@ -195,7 +222,9 @@ __global__ __launch_bounds__(128) void wgrad_cin1_kernel(
     }
     __syncthreads();
     if (tid < 32) {
-      for (int px = 0; px < WG_PT; ++px) bsum += lg[px * GS + tid];
+      float ts = 0.f;
+      for (int px = 0; px < WG_PT; ++px) ts += lg[px * GS + tid];
+      bsum += (double)ts;
     }
     for (int s = 0; s < WG_PT / 4; ++s) {
       const int px = 4 * s + kq;
@@ -213,7 +242,7 @@ __global__ __launch_bounds__(128) void wgrad_cin1_kernel(
       wpart[((size_t)slice * 9 + l16) * Cout + co] = acc[r];   // Cin == 1
     }
   }
-  if (tid < 32) bpart[(size_t)slice * Cout + tid] = bsum;
+  if (tid < 32) bpart[(size_t)slice * Cout + tid] = (float)bsum;
 }
 
 // ------------------------------------------------------------------ cout == 1 (last conv)
@@ -234,7 +263,7 @@ __global__ __launch_bounds__(128) void wgrad_cout1_kernel(
   const int tapi = l16 < 9 ? l16 : 0;
   const int tkh = tapi / 3, tkw = tapi % 3;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
+  double bsum = 0.0;
   const int t_beg = slice * g.tps, t_end = min(t_beg + g.tps, g.tiles);
   const int tpx = g.TH * g.TW;
   for (int t = t_beg; t < t_end; ++t) {
@@ -260,9 +289,11 @@ __global__ __launch_bounds__(128) void wgrad_cout1_kernel(
     }
     __syncthreads();
     if (tid == 0) {
+      float ts = 0.f;
       for (int img = 0; img < g.NI; ++img)
         for (int r = 0; r < g.TH; ++r)
-          for (int c = 0; c < g.TW; ++c) bsum += lgh[(img * HP + r + 1) * WP + c + 1];
+          for (int c = 0; c < g.TW; ++c) ts += lgh[(img * HP + r + 1) * WP + c + 1];
+      bsum += (double)ts;
     }
     for (int s = 0; s < WG_PT / 4; ++s) {
       const int px = 4 * s + kq;
@@ -280,33 +311,59 @@ __global__ __launch_bounds__(128) void wgrad_cout1_kernel(
     const int tap = kq * 4 + r;
     if (tap < 9) wpart[((size_t)slice * 9 + tap) * Cin + wave * 16 + l16] = acc[r];  // Cout == 1
   }
-  if (tid == 0) bpart[slice] = bsum;
+  if (tid == 0) bpart[slice] = (float)bsum;
 }
 
 // ------------------------------------------------------------------ slice reduction
-// thread per partial element (tap, co, ci) in [tap][co][ci] order (coalesced reads);
-// fixed-order sum over slices; scatter into the parameter-gradient layout.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ wpart, const float* __restrict__ bpart,
-                                    int S, float* __restrict__ dw, float* __restrict__ db,
-                                    int cin, int cout, int kind) {
-  const int nw = 9 * cout * cin;
+// Level 1: grid (element blocks, G slice groups); thread (e, g) sums slices
+// [g*S/G, (g+1)*S/G) in double (fixed order) -> work[g][e].  Level 2: thread per element
+// sums the G groups in order and scatters into the parameter-gradient layout.
+// Elements are [tap][co][ci] weights followed by the cout biases.
+__global__ void wgrad_reduce1_kernel(const float* __restrict__ wpart, const float* __restrict__ bpart,
+                                     int S, int G, double* __restrict__ work, int nw, int cout) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  const int E = nw + cout;
+  if (e >= E) return;
+  const int k0 = (int)((long)g * S / G), k1 = (int)((long)(g + 1) * S / G);
+  double s = 0.0;
   if (e < nw) {
-    float s = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < S; ++k) s += wpart[(size_t)k * nw + e];
+    for (int k = k0; k < k1; ++k) s += (double)wpart[(size_t)k * nw + e];
+  } else {
+    const int co = e - nw;
+    for (int k = k0; k < k1; ++k) s += (double)bpart[(size_t)k * cout + co];
+  }
+  work[(size_t)g * E + e] = s;
+}
+
+__global__ void wgrad_reduce2_kernel(const double* __restrict__ work, int G, float* __restrict__ dw,
+                                     float* __restrict__ db, int cin, int cout, int kind) {
+  const int nw = 9 * cout * cin;
+  const int E = nw + cout;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  double s = 0.0;
+  for (int g = 0; g < G; ++g) s += work[(size_t)g * E + e];
+  if (e < nw) {
     const int t = e / (cout * cin), rem = e - t * (cout * cin);
     const int co = rem / cin, ci = rem - co * cin;
     size_t idx;
     if (kind == 0) idx = ((size_t)co * cin + ci) * 9 + t;
     else idx = ((size_t)ci * cout + co) * 9 + (8 - t);
-    dw[idx] = s;
-  } else if (e < nw + cout && db) {
-    const int co = e - nw;
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += bpart[(size_t)k * cout + co];
-    db[co] = s;
+    dw[idx] = (float)s;
+  } else if (db) {
+    db[e - nw] = (float)s;
   }
+}
+
+static int reduce_groups(int slices, int cin, int cout) {
+  const int E = 9 * cin * cout + cout;
+  int G = 262144 / E;
+  if (G < 1) G = 1;
+  if (G > slices) G = slices;
+  if (G > 64) G = 64;
+  return G;
 }
 
 static size_t wg_lds(int variant, const WgGeom& g, int co_t) {
@@ -351,26 +408,42 @@ extern "C" int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, i
              cin, cout);
   if (cout == 32) {
     const size_t lds = wg_lds(0, g, 32);
-    auto k = wgrad_kernel<1>;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k, dim3(g.slices, 1, cin / 32), dim3(128), lds, s, src,
+    auto k = wgrad_kernel<1, 2>;
+    static bool attr1 = false;
+    if (!attr1) {
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr1 = true;
+    }
+    hipLaunchKernelGGL(k, dim3(g.slices, 1, cin / 32), dim3(256), lds, s, src,
                        (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cin, cout, g);
   } else {
     const size_t lds = wg_lds(0, g, 64);
-    auto k = wgrad_kernel<2>;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    auto k = wgrad_kernel<2, 1>;
+    static bool attr2 = false;
+    if (!attr2) {
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr2 = true;
+    }
     hipLaunchKernelGGL(k, dim3(g.slices, cout / 64, cin / 32), dim3(256), lds, s, src,
                        (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cin, cout, g);
   }
   return evh::check_launch("wgrad");
 }
 
+extern "C" size_t ebsdvae_wgrad_reduce_work(int slices, int cin, int cout) {
+  return (size_t)reduce_groups(slices, cin, cout) * (9 * (size_t)cin * cout + cout) * sizeof(double);
+}
+
 extern "C" int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
-                                    float* db, int cin, int cout, int kind,
+                                    float* db, int cin, int cout, int kind, void* work,
                                     ebsdvae_stream_t stream) {
-  EV_REQUIRE(wpart && dw && slices > 0, "wgrad_reduce: bad args");
-  const int n = 9 * cin * cout + cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     wpart, bpart, slices, dw, db, cin, cout, kind);
+  EV_REQUIRE(wpart && bpart && dw && work && slices > 0, "wgrad_reduce: bad args");
+  const int E = 9 * cin * cout + cout;
+  const int G = reduce_groups(slices, cin, cout);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3((E + 255) / 256, G), dim3(256), 0, st, wpart, bpart,
+                     slices, G, (double*)work, 9 * cin * cout, cout);
+  hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3((E + 255) / 256), dim3(256), 0, st,
+                     (const double*)work, G, dw, db, cin, cout, kind);
   return evh::check_launch("wgrad_reduce");
 }

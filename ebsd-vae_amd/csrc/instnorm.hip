@@ -85,9 +85,9 @@ static int in_bwd_tiles_host(int H, int W) {
 template <bool APPLY>
 __global__ __launch_bounds__(256) void in_bwd_kernel(
     const float* __restrict__ gnext, int pmode, const float* __restrict__ y,
-    const float2* __restrict__ st, const float2* __restrict__ bst, float2* __restrict__ part,
+    const float2* __restrict__ st, const float2* __restrict__ bst, double2* __restrict__ part,
     float* __restrict__ gy, int H, int W, int C, int T) {
-  __shared__ float4 red[2][256];
+  __shared__ double red[2][4][256];
   const int tile = blockIdx.x, b = blockIdx.y;
   const int CG = C >> 2;
   const int tid = threadIdx.x;
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) { m1[k] = bp[k].x; m2[k] = bp[k].y; }
   }
-  float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
+  double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
   const float* yb = y + (size_t)b * H * W * C;
   float* gyb = APPLY ? gy + (size_t)b * H * W * C : nullptr;
 
@@ -147,8 +147,8 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
         for (int ch = 0; ch < 4; ++ch) {
           const float x = xh[arg[ch]][ch];
           const float gx = gv[ch] * slope(x);
-          a1[ch] += gx;
-          a2[ch] = fmaf(gx, x, a2[ch]);
+          a1[ch] += (double)gx;
+          a2[ch] = fma((double)gx, (double)x, a2[ch]);
         }
       } else {
 #pragma unroll
@@ -187,8 +187,8 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
         const float x = (yy[ch] - mean[ch]) * rstd[ch];
         const float gx = gv[ch] * slope(x);
         if (!APPLY) {
-          a1[ch] += gx;
-          a2[ch] = fmaf(gx, x, a2[ch]);
+          a1[ch] += (double)gx;
+          a2[ch] = fma((double)gx, (double)x, a2[ch]);
         } else {
           o[ch] = rstd[ch] * (gx - m1[ch] - x * m2[ch]);
         }
@@ -197,37 +197,36 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
     }
   }
   if (!APPLY) {
-    red[0][tid] = make_float4(a1[0], a1[1], a1[2], a1[3]);
-    red[1][tid] = make_float4(a2[0], a2[1], a2[2], a2[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { red[0][k][tid] = a1[k]; red[1][k][tid] = a2[k]; }
     __syncthreads();
     if (tid < CG) {
-      float4 u = red[0][tid], v = red[1][tid];
+      double u[4], v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { u[k] = red[0][k][tid]; v[k] = red[1][k][tid]; }
       for (int r = 1; r < NPR; ++r) {
-        const float4 uu = red[0][r * CG + tid], vv = red[1][r * CG + tid];
-        u.x += uu.x; u.y += uu.y; u.z += uu.z; u.w += uu.w;
-        v.x += vv.x; v.y += vv.y; v.z += vv.z; v.w += vv.w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { u[k] += red[0][k][r * CG + tid]; v[k] += red[1][k][r * CG + tid]; }
       }
-      float2* o = part + ((size_t)b * T + tile) * C + c;
-      o[0] = make_float2(u.x, v.x);
-      o[1] = make_float2(u.y, v.y);
-      o[2] = make_float2(u.z, v.z);
-      o[3] = make_float2(u.w, v.w);
+      double2* o = part + ((size_t)b * T + tile) * C + c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = make_double2(u[k], v[k]);
     }
   }
 }
 
-__global__ void in_bwd_finalize_kernel(const float2* __restrict__ part, float2* __restrict__ bst,
-                                       int B, int C, int T, float inv_hw) {
+__global__ void in_bwd_finalize_kernel(const double2* __restrict__ part, float2* __restrict__ bst,
+                                       int B, int C, int T, double inv_hw) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * C) return;
   const int b = e / C, c = e - b * C;
-  float s1 = 0.f, s2 = 0.f;
+  double s1 = 0.0, s2 = 0.0;
   for (int t = 0; t < T; ++t) {
-    const float2 v = part[((size_t)b * T + t) * C + c];
+    const double2 v = part[((size_t)b * T + t) * C + c];
     s1 += v.x;
     s2 += v.y;
   }
-  bst[e] = make_float2(s1 * inv_hw, s2 * inv_hw);
+  bst[e] = make_float2((float)(s1 * inv_hw), (float)(s2 * inv_hw));
 }
 
 static int grid_for(size_t n4) {
@@ -277,7 +276,7 @@ extern "C" int ebsdvae_in_bwd_tiles(int H, int W, int C) {
 }
 
 extern "C" int ebsdvae_in_bwd_reduce(const float* gnext, int pmode, const float* y,
-                                     const float* stats, float* part, int B, int H, int W, int C,
+                                     const float* stats, double* part, int B, int H, int W, int C,
                                      ebsdvae_stream_t stream) {
   EV_REQUIRE(gnext && y && stats && part, "in_bwd_reduce: null pointer");
   EV_REQUIRE(pmode >= 0 && pmode <= 2 && C % 4 == 0 && C <= 1024 && (256 % (C / 4)) == 0,
@@ -285,18 +284,18 @@ extern "C" int ebsdvae_in_bwd_reduce(const float* gnext, int pmode, const float*
   EV_REQUIRE(pmode != P_POOL || ((H | W) & 1) == 0, "in_bwd_reduce: pool needs even H, W");
   const int T = in_bwd_tiles_host(H, W);
   hipLaunchKernelGGL(in_bwd_kernel<false>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
-                     pmode, y, (const float2*)stats, (const float2*)nullptr, (float2*)part,
+                     pmode, y, (const float2*)stats, (const float2*)nullptr, (double2*)part,
                      (float*)nullptr, H, W, C, T);
   return evh::check_launch("in_bwd_reduce");
 }
 
-extern "C" int ebsdvae_in_bwd_finalize(const float* part, float* bstats, int B, int C, int tiles,
+extern "C" int ebsdvae_in_bwd_finalize(const double* part, float* bstats, int B, int C, int tiles,
                                        int HW, ebsdvae_stream_t stream) {
   EV_REQUIRE(part && bstats, "in_bwd_finalize: null pointer");
   const int n = B * C;
   hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, (const float2*)part, (float2*)bstats, B, C, tiles,
-                     1.0f / (float)HW);
+                     (hipStream_t)stream, (const double2*)part, (float2*)bstats, B, C, tiles,
+                     1.0 / (double)HW);
   return evh::check_launch("in_bwd_finalize");
 }
 
@@ -307,7 +306,7 @@ extern "C" int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* 
   EV_REQUIRE(pmode >= 0 && pmode <= 2 && C % 4 == 0 && (256 % (C / 4)) == 0, "in_bwd_apply: bad pmode/C");
   const int T = in_bwd_tiles_host(H, W);
   hipLaunchKernelGGL(in_bwd_kernel<true>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
-                     pmode, y, (const float2*)stats, (const float2*)bstats, (float2*)nullptr, gy, H,
+                     pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy, H,
                      W, C, T);
   return evh::check_launch("in_bwd_apply");
 }

@@ -32,7 +32,8 @@ SIGNATURES = {
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],
     "ebsdvae_conv3x3_wgrad_slices": [I, I, I, I, I],
     "ebsdvae_conv3x3_wgrad": [P, P, I, P, P, P, I, I, I, I, I, P],
-    "ebsdvae_wgrad_reduce": [P, P, I, P, P, I, I, I, P],
+    "ebsdvae_wgrad_reduce_work": [I, I, I],
+    "ebsdvae_wgrad_reduce": [P, P, I, P, P, I, I, I, P, P],
     "ebsdvae_in_stats_finalize": [P, P, I, I, I, I, P],
     "ebsdvae_act_apply": [P, P, I, P, I, I, I, I, P],
     "ebsdvae_in_bwd_tiles": [I, I, I],
@@ -52,10 +53,10 @@ SIGNATURES = {
     "ebsdvae_vae_loss_bwd": [P, P, P, P, P, F, P, P, P, P, F, P, P, P, P, P, I, I, I, P],
     "ebsdvae_adam": [P, P, P, P, P, P, I64, F, F, F, F, F, I, P],
 }
-_RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p}
+_RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t}
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
-           "ebsdvae_in_bwd_tiles"}
+           "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work"}
 
 _lib = None
 _lock = threading.Lock()

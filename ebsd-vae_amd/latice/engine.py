@@ -95,6 +95,53 @@ def build_plan(inplanes: int = 32, latent_dim: int = 16, image_size: int = 128) 
     return Plan(inplanes, latent_dim, image_size, tuple(enc), tuple(dec))
 
 
+# ----------------------------------------------------------------------------- probes
+_PROBE = None
+
+
+class probe:
+    """Record HIP events around the conv kernel launches (bench.py's live per-kernel
+    timing): records (family, algorithmic_flops, ev_start, ev_end) on the current stream."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _PROBE
+        _PROBE = self.records
+        return self
+
+    def __exit__(self, *exc):
+        global _PROBE
+        _PROBE = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for fam, flops, e0, e1 in self.records:
+            d = out.setdefault(fam, {"launches": 0, "flops": 0.0, "ms": 0.0})
+            d["launches"] += 1
+            d["flops"] += flops
+            d["ms"] += e0.elapsed_time(e1)
+        return out
+
+
+def _launch(family, flops, fn, *args):
+    if _PROBE is None:
+        return fn(*args)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    r = fn(*args)
+    e1.record()
+    _PROBE.append((family, float(flops), e0, e1))
+    return r
+
+
+def conv_flops(B, H, W, cin, cout):
+    return 2.0 * B * H * W * cin * cout * 9
+
+
 # ----------------------------------------------------------------------------- helpers
 def _empty(*shape, like):
     return torch.empty(shape, dtype=torch.float32, device=like.device)
@@ -115,8 +162,9 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B):
     y = _empty(B, H, H, layer.cout, like=w)
     T = N.call("ebsdvae_conv3x3_stat_tiles", H, H, layer.cout)
     part = _empty(B, T, layer.cout, 2, like=w)
-    N.call("ebsdvae_conv3x3_fwd", N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp), N.ptr(b),
-           N.ptr(y), N.ptr(part), B, H, H, layer.cin, layer.cout, N.stream())
+    _launch("conv3x3_fwd", conv_flops(B, H, H, layer.cin, layer.cout), N.call,
+            "ebsdvae_conv3x3_fwd", N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp), N.ptr(b),
+            N.ptr(y), N.ptr(part), B, H, H, layer.cin, layer.cout, N.stream())
     st = _empty(B, layer.cout, 2, like=w)
     N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
            N.stream())
@@ -127,12 +175,12 @@ def in_backward(gnext, pmode, y, st):
     """gy = d loss / d y through [pool|up] . lrelu . InstanceNorm of one block."""
     B, H, W, C = y.shape
     T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
-    part = _empty(B, T, C, 2, like=y)
+    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
     s = N.stream()
-    N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(part),
+    N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), part.data_ptr(),
            B, H, W, C, s)
     bst = _empty(B, C, 2, like=y)
-    N.call("ebsdvae_in_bwd_finalize", N.ptr(part), N.ptr(bst), B, C, T, H * W, s)
+    N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, T, H * W, s)
     gy = torch.empty_like(y)
     N.call("ebsdvae_in_bwd_apply", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
            N.ptr(gy), B, H, W, C, s)
@@ -147,18 +195,22 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
     wpart = _empty(S_, 9, cout, cin, like=gy)
     bpart = _empty(S_, cout, like=gy)
     s = N.stream()
-    N.call("ebsdvae_conv3x3_wgrad", N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(gy),
-           N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout, s)
+    _launch("conv3x3_wgrad", conv_flops(B, H, W, cin, cout), N.call,
+            "ebsdvae_conv3x3_wgrad", N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(gy),
+            N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout, s)
+    nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
+    work = torch.empty(nbytes // 8, dtype=torch.float64, device=gy.device)
     N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db),
-           cin, cout, kind, s)
+           cin, cout, kind, work.data_ptr(), s)
 
 
 def conv_dgrad(gy, layer: ConvLayer, w):
     B, H, W, _ = gy.shape
     wd = pack_weight(w, layer, dgrad=True)
     gin = _empty(B, H, W, layer.cin, like=gy)
-    N.call("ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(wd), None, N.ptr(gin), None,
-           B, H, W, layer.cout, layer.cin, N.stream())
+    _launch("conv3x3_fwd", conv_flops(B, H, W, layer.cin, layer.cout), N.call,
+            "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(wd), None, N.ptr(gin), None,
+            B, H, W, layer.cout, layer.cin, N.stream())
     return gin
 
 

@@ -1,0 +1,164 @@
+"""Training-step driver for the MI355X path: the work of
+`VAELightningModule.training_step` + `loss.backward()` + `optimizer.step()`
+(latice/lightning_module.py:248-273, :359-369) without autograd bookkeeping, and the
+data-parallel version of it that the reference only gets implicitly from Lightning DDP.
+
+* Parameters are re-pointed into ONE flat fp32 buffer and gradients are written by the
+  kernels straight into ONE flat gradient buffer (ordered decoder -> heads -> encoder, the
+  order in which the backward finishes them), so the optimiser is a single fused Adam
+  launch and the gradient exchange is two contiguous RCCL all-reduces.
+* Data parallelism (one process per GPU, torch.distributed "nccl" == RCCL over xGMI):
+  every rank processes its own batch shard; the loss gradient is pre-scaled by 1/W so a
+  SUM all-reduce yields the mean gradient with no extra pass.  Bucket 0 (decoder + heads,
+  complete after the decoder backward) is all-reduced asynchronously while the encoder
+  backward runs; bucket 1 follows.  7.4 MB per step in total (1.85M fp32 parameters).
+* N == 1: the whole step can be captured into a hipGraph (capture()/replay()).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _native as N
+from . import engine as E
+from .functional import dec_param_names, enc_param_names
+
+
+class GradReducer:
+    """Two-bucket asynchronous SUM all-reduce of a flat gradient buffer."""
+
+    def __init__(self, gflat: torch.Tensor, split: int, group=None):
+        self.gflat, self.split, self.group = gflat, split, group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self._works = []
+
+    def start(self, bucket: int):
+        if self.world == 1:
+            return
+        t = self.gflat[: self.split] if bucket == 0 else self.gflat[self.split:]
+        self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def finish(self):
+        for w in self._works:
+            w.wait()
+        self._works = []
+
+
+def shard_batch(x: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    """Contiguous 1/W slice of a global batch."""
+    B = x.shape[0]
+    if B % world:
+        raise ValueError(f"global batch {B} not divisible by world size {world}")
+    per = B // world
+    return x[rank * per:(rank + 1) * per]
+
+
+class VAETrainer:
+    def __init__(self, model, kl_lambda: float = 5e-6, lr: float = 1e-4, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, amsgrad: bool = False,
+                 seed: int = 0, group=None):
+        self.model = model
+        self.plan = model.plan
+        self.kl_lambda = float(kl_lambda)
+        self.lr, self.betas, self.adam_eps = float(lr), betas, float(eps)
+        self.weight_decay, self.amsgrad = float(weight_decay), bool(amsgrad)
+        self.seed = int(seed)
+        params = dict(model.named_parameters())
+        dev = next(iter(params.values())).device
+        if dev.type != "cuda":
+            raise RuntimeError("VAETrainer needs the model on a ROCm device (no CPU fallback)")
+        dec = dec_param_names(self.plan) + list(E.HEAD_NAMES)
+        enc = enc_param_names(self.plan)
+        order = dec + enc
+        if set(order) != set(params):
+            raise RuntimeError("unexpected parameter set")
+        total = sum(params[n].numel() for n in order)
+        self.flat = torch.empty(total, device=dev, dtype=torch.float32)
+        self.gflat = torch.zeros(total, device=dev, dtype=torch.float32)
+        self.P, self.G = {}, {}
+        off = 0
+        with torch.no_grad():
+            for n in order:
+                p = params[n]
+                k = p.numel()
+                view = self.flat[off:off + k].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                self.P[n] = p
+                self.G[n] = self.gflat[off:off + k].view_as(p)
+                off += k
+        self.split = sum(params[n].numel() for n in dec)
+        self.exp_avg = torch.zeros_like(self.flat)
+        self.exp_avg_sq = torch.zeros_like(self.flat)
+        self.max_exp_avg_sq = torch.zeros_like(self.flat) if self.amsgrad else None
+        self.step_count = torch.zeros((), device=dev, dtype=torch.float32)
+        self.one = torch.ones((), device=dev, dtype=torch.float32)
+        self.noise_counter = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.reducer = GradReducer(self.gflat, self.split, group)
+        self.world = self.reducer.world
+        self._eps = None
+        self.graph = None
+        self._static = None
+
+    @property
+    def numel(self) -> int:
+        return self.flat.numel()
+
+    def _noise(self, B):
+        L = self.plan.latent_dim
+        if self._eps is None or self._eps.shape[0] != B:
+            self._eps = torch.empty(B, L, device=self.flat.device, dtype=torch.float32)
+        return E.normal_(self._eps, self.seed, counter=self.noise_counter)
+
+    def forward_backward(self, x: torch.Tensor, eps: torch.Tensor | None = None):
+        """fwd + loss + bwd into self.gflat (+ the DP gradient exchange).  Returns the three
+        loss scalars (device tensors)."""
+        plan, P, G = self.plan, self.P, self.G
+        enc, se = E.encoder_forward(plan, x, P)
+        eps = self._noise(x.shape[0]) if eps is None else eps
+        flat, mu, std, z, dec_in = E.heads_forward(plan, enc, P, eps)
+        x_hat, sd = E.decoder_forward(plan, dec_in, P)
+        (loss, kl, rec), _ = E.loss_forward(x_hat, x, z, mu, std, self.kl_lambda)
+        g_xhat, g_z, g_mu, g_std, _ = E.loss_backward(x_hat, x, z, mu, std, self.kl_lambda,
+                                                      g_loss=self.one, scale=1.0 / self.world)
+        _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G)
+        g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P, grads=G)
+        self.reducer.start(0)
+        E.encoder_backward(plan, g_enc, x, se, P, grads=G)
+        self.reducer.start(1)
+        self.reducer.finish()
+        return loss, kl, rec
+
+    def optimizer_step(self):
+        b1, b2 = self.betas
+        N.call("ebsdvae_adam", N.ptr(self.flat), N.ptr(self.gflat), N.ptr(self.exp_avg),
+               N.ptr(self.exp_avg_sq), N.ptr(self.max_exp_avg_sq), N.ptr(self.step_count),
+               self.flat.numel(), self.lr, float(b1), float(b2), self.adam_eps, self.weight_decay,
+               int(self.amsgrad), N.stream())
+
+    def step(self, x: torch.Tensor, eps: torch.Tensor | None = None):
+        out = self.forward_backward(x, eps)
+        self.optimizer_step()
+        return out
+
+    # ------------------------------------------------------------------ hipGraph (N == 1)
+    def capture(self, x: torch.Tensor, warmup: int = 1):
+        """Capture one whole step on static input `x` (N == 1 only: collectives stay out
+        of graphs).  Warm-up steps run first on a side stream, as torch requires."""
+        if self.world != 1:
+            raise RuntimeError("graph capture is for single-process runs")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step(x)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = self.step(x)
+        self.graph, self._static = g, (x, out)
+        return out
+
+    def replay(self):
+        self.graph.replay()
+        return self._static[1]

@@ -26,6 +26,7 @@
 #ifndef EBSDVAE_H_
 #define EBSDVAE_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -78,8 +79,11 @@ int ebsdvae_conv3x3_wgrad_slices(int B, int H, int W, int cin, int cout);
 int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, int src_mode,
                           const float* gy, float* wpart, float* bpart, int B, int H, int W,
                           int cin, int cout, ebsdvae_stream_t stream);
+/* work: device scratch of ebsdvae_wgrad_reduce_work(...) bytes (double partial sums) */
+size_t ebsdvae_wgrad_reduce_work(int slices, int cin, int cout);
 int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
-                         float* db, int cin, int cout, int kind, ebsdvae_stream_t stream);
+                         float* db, int cin, int cout, int kind, void* work,
+                         ebsdvae_stream_t stream);
 
 /* ---- InstanceNorm2d + LeakyReLU (latice/model.py:96-97,105-106) -----------------------
  * combine conv-epilogue partials {mean,M2} (tiles per image, n elements each) into
@@ -94,11 +98,13 @@ int ebsdvae_act_apply(const float* src, const float* src_stats, int src_mode, fl
  * gnext: gradient w.r.t. the consumer's input; pmode 0 identity, 1 the consumer pooled
  * (gnext at H/2), 2 the consumer upsampled (gnext at 2H).  y/stats: the block's saved
  * pre-norm output and statistics.  Two passes: reduce -> bstats {mean(g_xhat),
- * mean(g_xhat*xhat)} per (b,c), then apply -> gy (conv-output gradient, (B,H,W,C)). */
+ * mean(g_xhat*xhat)} per (b,c), then apply -> gy (conv-output gradient, (B,H,W,C)).
+ * The plane sums are accumulated in double (part: B*tiles*C double2), as the reference's
+ * CPU InstanceNorm backward does; the mean-subtraction cancels strongly. */
 int ebsdvae_in_bwd_tiles(int H, int W, int C);
 int ebsdvae_in_bwd_reduce(const float* gnext, int pmode, const float* y, const float* stats,
-                          float* part, int B, int H, int W, int C, ebsdvae_stream_t stream);
-int ebsdvae_in_bwd_finalize(const float* part, float* bstats, int B, int C, int tiles,
+                          double* part, int B, int H, int W, int C, ebsdvae_stream_t stream);
+int ebsdvae_in_bwd_finalize(const double* part, float* bstats, int B, int C, int tiles,
                             int HW, ebsdvae_stream_t stream);
 int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* y, const float* stats,
                          const float* bstats, float* gy, int B, int H, int W, int C,

@@ -136,14 +136,15 @@ def nchw_unflatten(f: np.ndarray, c: int, s: int) -> np.ndarray:
 
 
 # ----------------------------------------------------------------------------- model
-def _params64(sd):
-    return {k: np.asarray(v, np.float64) for k, v in sd.items()}
+def _params(sd, dtype):
+    return {k: np.asarray(v, dtype) for k, v in sd.items()}
 
 
-def forward(sd, x_nchw: np.ndarray, eps: np.ndarray):
-    """Full forward. Returns (outputs dict, cache for backward)."""
-    p = _params64(sd)
-    x = np.asarray(x_nchw, np.float64).transpose(0, 2, 3, 1)
+def forward(sd, x_nchw: np.ndarray, eps: np.ndarray, dtype=np.float64):
+    """Full forward. Returns (outputs dict, cache for backward).  dtype=np.float32 runs the
+    same algorithm in single precision (used to measure generic fp32 noise)."""
+    p = _params(sd, dtype)
+    x = np.asarray(x_nchw, dtype).transpose(0, 2, 3, 1)
     cache = {"x": x, "enc": [], "dec": []}
     a = x
     for i, idx in enumerate(ENC_IDX):
@@ -162,7 +163,7 @@ def forward(sd, x_nchw: np.ndarray, eps: np.ndarray):
     mu = flat @ p["mu.0.weight"].T + p["mu.0.bias"]
     logvar = flat @ p["logvar.0.weight"].T + p["logvar.0.bias"]
     std = np.exp(logvar / 2)
-    e = np.asarray(eps, np.float64)
+    e = np.asarray(eps, dtype)
     z = mu + e * std
     out = z @ p["linear2.0.weight"].T + p["linear2.0.bias"]
     a = nchw_unflatten(out, c, s)

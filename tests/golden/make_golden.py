@@ -161,6 +161,22 @@ def run_case(ref_model, ref_lm, seeding, *, name, batch, image_size=128, latent_
         out["grad_names"] = np.array(names)
         out["grad_norms"] = np.array(norms)
         out["ref_f32_grad_dev"] = np.array(fdev)
+        # a second, independent fp32 implementation of the same algorithm: the repo's numpy
+        # oracle run in float32 (oracle/vae_oracle.py, dtype=np.float32).  Its deviation from
+        # fp64 measures the fp32 noise floor of these gradients (max-pool argmax near-ties and
+        # LeakyReLU sign flips at xhat ~ 0 route gradient discretely; InstanceNorm backward
+        # cancels strongly).
+        sys.path.insert(0, REPO)
+        from oracle import vae_oracle as VO
+        _, c32 = VO.forward(sd, x, eps, dtype=np.float32)
+        g32 = VO.backward(c32, x, kl_lambda)
+        ndev, nabs = [], []
+        for pname, p in r["model"].named_parameters():
+            g = p.grad.detach().numpy()
+            ndev.append(float(np.abs(g32[pname] - g).max() / max(np.abs(g).max(), 1e-30)))
+            nabs.append(float(np.abs(g32[pname] - g).max()))
+        out["oracle_f32_grad_dev"] = np.array(ndev)
+        out["oracle_f32_grad_absdev"] = np.array(nabs)
     path = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(path, **out)
     print(f"wrote {path}  ({os.path.getsize(path) / 1024:.0f} KiB)  loss={float(out['loss']):.8f} "
