@@ -40,6 +40,7 @@ static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
     if (g->NI * H * W != WG_PT) return false;
   }
   if (W % g->TW || H % g->TH) return false;
+  if (g->NI * (g->TH + 2) * (g->TW + 2) > 224) return false;   // KH = 7 halo items / thread
   g->ntx = W / g->TW;
   g->nty = H / g->TH;
   const long imgs = (B + g->NI - 1) / g->NI;
@@ -64,15 +65,24 @@ EV_DEVINL void tile_origin(int t, const WgGeom& g, int& b0, int& y0, int& x0) {
 }
 
 // ------------------------------------------------------------------ generic (cin % 32 == 0)
-template <int NWCO, int KSPLIT>
+// Software-pipelined over the slice's pixel tiles: the NEXT tile's gy rows and raw
+// activation halo (+ its InstanceNorm stats) are loaded into registers while the MFMAs of
+// the current tile run; the transform (InstanceNorm + LeakyReLU [+ upsample]) is applied
+// when they are written to LDS.  MODE is never NORM_POOL here: pool-fed layers pass the
+// pooled activation that their forward conv materialised (RAW).
+template <int NWCO, int KSPLIT, int MODE>
 __global__ __launch_bounds__(256) void wgrad_kernel(
-    const float* __restrict__ src, const float2* __restrict__ sstats, int smode,
+    const float* __restrict__ src, const float2* __restrict__ sstats,
     const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
     int H, int W, int Cin, int Cout, WgGeom g) {
   constexpr int CO_T = NWCO * 32;
   constexpr int GS = CO_T + 16;
-  constexpr int NT = 256;
+  constexpr int KG = CO_T / 8;    // gy float4 items per thread per tile
+  constexpr int KH = 7;           // halo float4 items per thread per tile (upper bound)
+  constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_UP);
+  constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
   static_assert(NWCO * 2 * KSPLIT == 4, "4 waves per block");
+  static_assert(MODE != ACT_NORM_POOL, "pool-fed layers use the materialised activation");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lg = smem;                 // [128][GS]
   float* la = smem + WG_PT * GS;    // [halo px][48]
@@ -81,6 +91,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(
   const int slice = blockIdx.x, co0 = blockIdx.y * CO_T, ci0 = blockIdx.z * 32;
   const int HP = g.TH + 2, WP = g.TW + 2, halo = g.NI * HP * WP;
   const int l16 = lane & 15, kq = lane >> 4;
+  const int Hs = UPS ? H / 2 : H, Ws = UPS ? W / 2 : W;
+  const int qh = tid & 7;           // this thread's 4-channel group of every halo pixel
+  const int qg = tid % (CO_T / 4);  // this thread's 4-channel group of every gy pixel
 
   f32x4 acc[2][9];
 #pragma unroll
@@ -92,32 +105,77 @@ __global__ __launch_bounds__(256) void wgrad_kernel(
   const int t_beg = slice * g.tps;
   const int t_end = min(t_beg + g.tps, g.tiles);
   const int tpx = g.TH * g.TW;
-  for (int t = t_beg; t < t_end; ++t) {
+  float4 rg[KG], rh[KH];
+  float2 st[2][4];
+  int cb0 = 0, cy0 = 0, cx0 = 0;   // origin of the tile held in registers
+  auto issue = [&](int t) {
     int b0, y0, x0;
     tile_origin(t, g, b0, y0, x0);
-    __syncthreads();
-    // gy tile: 128 px x CO_T channels
-    for (int i = tid; i < WG_PT * CO_T / 4; i += NT) {
-      const int px = i / (CO_T / 4), q = i - px * (CO_T / 4);
+    cb0 = b0; cy0 = y0; cx0 = x0;
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const int px = (tid + 256 * k) / (CO_T / 4);
       const int img = px / tpx, rem = px - img * tpx;
       const int r = rem / g.TW, c = rem - r * g.TW;
       const int gb = b0 + img;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gb < B) v = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + q * 4);
-      st4(lg + px * GS + q * 4, v);
+      if (gb < B) rg[k] = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + qg * 4);
     }
-    // activation halo: halo px x 32 channels
-    for (int i = tid; i < halo * 8; i += NT) {
-      const int pix = i >> 3, q = i & 7;
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      const int pix = (tid + 256 * k) >> 3;
       const int img = pix / (HP * WP), rem = pix - img * (HP * WP);
       const int hh = rem / WP, ww = rem - hh * WP;
       const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W)
-        v = load_act4(src, sstats, smode, gb, gh, gw, ci0 + q * 4, H, W, Cin);
-      st4(la + pix * WG_AS + q * 4, v);
+      if (pix < halo && gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
+        const int sh = UPS ? (gh >> 1) : gh, sw = UPS ? (gw >> 1) : gw;
+        rh[k] = ld4(src + (((size_t)gb * Hs + sh) * Ws + sw) * Cin + ci0 + qh * 4);
+      }
     }
+    if (NORM) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int gb = min(b0 + i, B - 1);
+        const float2* sp = sstats + (size_t)gb * Cin + ci0 + qh * 4;
+        st[i][0] = sp[0]; st[i][1] = sp[1]; st[i][2] = sp[2]; st[i][3] = sp[3];
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const int px = (tid + 256 * k) / (CO_T / 4);
+      const int img = px / tpx;
+      float4 v = rg[k];
+      if (cb0 + img >= B) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      st4(lg + px * GS + qg * 4, v);
+    }
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      const int pix = (tid + 256 * k) >> 3;
+      if (pix < halo) {
+        const int img = pix / (HP * WP), rem = pix - img * (HP * WP);
+        const int hh = rem / WP, ww = rem - hh * WP;
+        const int gh = cy0 + hh - 1, gw = cx0 + ww - 1, gb = cb0 + img;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
+          v = rh[k];
+          if (NORM) {
+            const float2* s4 = st[img > 0 ? 1 : 0];
+            v = make_float4(normact(v.x, s4[0]), normact(v.y, s4[1]), normact(v.z, s4[2]),
+                            normact(v.w, s4[3]));
+          }
+        }
+        st4(la + pix * WG_AS + qh * 4, v);
+      }
+    }
+  };
+
+  if (t_beg < t_end) issue(t_beg);
+  for (int t = t_beg; t < t_end; ++t) {
     __syncthreads();
+    store();
+    __syncthreads();
+    if (t + 1 < t_end) issue(t + 1);
     if (blockIdx.z == 0 && tid < CO_T) {
       float ts = 0.f;
       for (int px = 0; px < WG_PT; ++px) ts += lg[px * GS + tid];
@@ -373,6 +431,20 @@ static size_t wg_lds(int variant, const WgGeom& g, int co_t) {
   return (WG_PT * 48 + halo) * sizeof(float);
 }
 
+template <int NWCO, int KSPLIT, int MODE>
+static void launch_wg(dim3 grid, size_t lds, hipStream_t s, const float* src, const float* st,
+                      const float* gy, float* wpart, float* bpart, int B, int H, int W, int cin,
+                      int cout, const WgGeom& g) {
+  auto k = wgrad_kernel<NWCO, KSPLIT, MODE>;
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, (const float2*)st, gy, wpart, bpart, B, H, W,
+                     cin, cout, g);
+}
+
 }  // namespace ev
 
 using namespace ev;
@@ -406,26 +478,26 @@ extern "C" int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, i
   }
   EV_REQUIRE(cin % 32 == 0 && (cout == 32 || cout % 64 == 0), "conv3x3_wgrad: cin=%d cout=%d unsupported",
              cin, cout);
+  EV_REQUIRE(src_mode != ACT_NORM_POOL,
+             "conv3x3_wgrad: pass the pooled activation materialised by the forward (RAW)");
   if (cout == 32) {
     const size_t lds = wg_lds(0, g, 32);
-    auto k = wgrad_kernel<1, 2>;
-    static bool attr1 = false;
-    if (!attr1) {
-      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr1 = true;
+    const dim3 grid(g.slices, 1, cin / 32);
+    switch (src_mode) {
+      case ACT_RAW: launch_wg<1, 2, ACT_RAW>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_NORM: launch_wg<1, 2, ACT_NORM>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_UP: launch_wg<1, 2, ACT_UP>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      default: launch_wg<1, 2, ACT_NORM_UP>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
     }
-    hipLaunchKernelGGL(k, dim3(g.slices, 1, cin / 32), dim3(256), lds, s, src,
-                       (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cin, cout, g);
   } else {
     const size_t lds = wg_lds(0, g, 64);
-    auto k = wgrad_kernel<2, 1>;
-    static bool attr2 = false;
-    if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr2 = true;
+    const dim3 grid(g.slices, cout / 64, cin / 32);
+    switch (src_mode) {
+      case ACT_RAW: launch_wg<2, 1, ACT_RAW>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_NORM: launch_wg<2, 1, ACT_NORM>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_UP: launch_wg<2, 1, ACT_UP>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      default: launch_wg<2, 1, ACT_NORM_UP>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
     }
-    hipLaunchKernelGGL(k, dim3(g.slices, cout / 64, cin / 32), dim3(256), lds, s, src,
-                       (const float2*)src_stats, src_mode, gy, wpart, bpart, B, H, W, cin, cout, g);
   }
   return evh::check_launch("wgrad");
 }

@@ -26,7 +26,7 @@ SIGNATURES = {
     "ebsdvae_last_error": [],
     "ebsdvae_version": [],
     "ebsdvae_pack_conv_weight": [P, P, I, I, I, I, P],
-    "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_stat_tiles": [I, I, I],
     "ebsdvae_conv3x3_cout1_fwd": [P, P, I, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],

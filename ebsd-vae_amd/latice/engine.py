@@ -155,19 +155,24 @@ def pack_weight(w, layer: ConvLayer, dgrad: bool):
     return out
 
 
-def conv_forward(src, src_stats, layer: ConvLayer, w, b, B):
-    """One conv block forward: y (B,H,H,cout) pre-norm + IN stats {mean,rstd} (B,cout,2)."""
+def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False):
+    """One conv block forward: y (B,H,H,cout) pre-norm + IN stats {mean,rstd} (B,cout,2).
+    keep_act: also return the conv's logical input (materialised by the kernel), used by
+    max-pool-fed layers so their wgrad reads the pooled tensor."""
     H = layer.H
     wp = pack_weight(w, layer, dgrad=False)
     y = _empty(B, H, H, layer.cout, like=w)
     T = N.call("ebsdvae_conv3x3_stat_tiles", H, H, layer.cout)
     part = _empty(B, T, layer.cout, 2, like=w)
+    act = _empty(B, H, H, layer.cin, like=w) if keep_act else None
     _launch("conv3x3_fwd", conv_flops(B, H, H, layer.cin, layer.cout), N.call,
             "ebsdvae_conv3x3_fwd", N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp), N.ptr(b),
-            N.ptr(y), N.ptr(part), B, H, H, layer.cin, layer.cout, N.stream())
+            N.ptr(y), N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout, N.stream())
     st = _empty(B, layer.cout, 2, like=w)
     N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
            N.stream())
+    if keep_act:
+        return y, st, act
     return y, st
 
 
@@ -210,7 +215,7 @@ def conv_dgrad(gy, layer: ConvLayer, w):
     gin = _empty(B, H, W, layer.cin, like=gy)
     _launch("conv3x3_fwd", conv_flops(B, H, W, layer.cin, layer.cout), N.call,
             "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(wd), None, N.ptr(gin), None,
-            B, H, W, layer.cout, layer.cin, N.stream())
+            None, B, H, W, layer.cout, layer.cin, N.stream())
     return gin
 
 
@@ -227,7 +232,12 @@ def encoder_forward(plan: Plan, x, params):
     saved = {}
     src, sst = x, None
     for L in plan.enc:
-        y, st = conv_forward(src, sst, L, params[L.name + ".weight"], params[L.name + ".bias"], B)
+        w, b = params[L.name + ".weight"], params[L.name + ".bias"]
+        if L.src_mode == ACT_NORM_POOL:
+            y, st, act = conv_forward(src, sst, L, w, b, B, keep_act=True)
+            saved[L.name + ".act_in"] = act
+        else:
+            y, st = conv_forward(src, sst, L, w, b, B)
         saved[L.name] = (y, st)
         src, sst = y, st
     s, C = plan.enc_side, plan.enc_channels
@@ -246,14 +256,17 @@ def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=Fa
         L = plan.enc[i]
         y, st = saved[L.name]
         gy = in_backward(g_next, L.pmode, y, st)
+        mode = L.src_mode
         if i == 0:
             src, sst = x, None
+        elif L.src_mode == ACT_NORM_POOL:
+            src, sst, mode = saved[L.name + ".act_in"], None, ACT_RAW
         else:
             src, sst = saved[plan.enc[i - 1].name]
         wn, bn = L.name + ".weight", L.name + ".bias"
         dw = _grad_buf(grads, wn, params[wn])
         db = _grad_buf(grads, bn, params[bn])
-        conv_wgrad(src, sst, L.src_mode, gy, L.cin, L.cout, L.kind, dw, db)
+        conv_wgrad(src, sst, mode, gy, L.cin, L.cout, L.kind, dw, db)
         out[wn], out[bn] = dw, db
         if i > 0:
             g_next = conv_dgrad(gy, L, params[wn])

@@ -41,7 +41,7 @@ int ebsdvae_version(void);
 /* ---- weights ------------------------------------------------------------------------
  * Pack a Conv2d (kind 0: (cout,cin,3,3), latice/model.py:95,148) or ConvTranspose2d
  * (kind 1: (cin,cout,3,3), latice/model.py:102-104) weight into the kernel layout
- * [tap][Cin'][Cout'].  for_dgrad=0: the forward conv (Cin'=cin, Cout'=cout);
+ * [Cin'/8][tap][8][Cout'] (one contiguous slab per 8-channel K chunk).  for_dgrad=0: the forward conv (Cin'=cin, Cout'=cout);
  * for_dgrad=1: the input-gradient conv (Cin'=cout, Cout'=cin, taps flipped). */
 int ebsdvae_pack_conv_weight(const float* src, float* dst, int cin, int cout, int kind,
                              int for_dgrad, ebsdvae_stream_t stream);
@@ -51,12 +51,15 @@ int ebsdvae_pack_conv_weight(const float* src, float* dst, int cin, int cout, in
  * (zero padding 1).  Replaces nn.Conv2d / nn.ConvTranspose2d forward
  * (latice/model.py:95,102-104) and, with a for_dgrad pack and RAW source, their input
  * gradients.  If stat_part != NULL, also writes per-tile InstanceNorm partials
- * {mean, M2} per (b, tile, co) (count ebsdvae_conv3x3_stat_tiles per image).
- * cin in {1} U {32k}, cout in {32, 64, 128}; W <= tile width (128x128 and 256x256 nets).
- * bias may be NULL. */
+ * {mean, M2} per (b, tile, co) (count ebsdvae_conv3x3_stat_tiles per image).  If
+ * act_out != NULL, also writes the conv's logical input act(src) as (B,H,W,cin) NHWC (used
+ * for max-pool-fed layers, whose weight gradient then reads the 4x smaller pooled tensor).
+ * cin in {1} U {8k}, cout in {32, 64, 128}; W <= tile width (128x128 and 256x256 nets).
+ * bias may be NULL.  wpack layout: [cin/8][tap][8][cout] (ebsdvae_pack_conv_weight). */
 int ebsdvae_conv3x3_fwd(const float* src, const float* src_stats, int src_mode,
                         const float* wpack, const float* bias, float* y, float* stat_part,
-                        int B, int H, int W, int cin, int cout, ebsdvae_stream_t stream);
+                        float* act_out, int B, int H, int W, int cin, int cout,
+                        ebsdvae_stream_t stream);
 int ebsdvae_conv3x3_stat_tiles(int H, int W, int cout);
 
 /* 3x3 conv with a single output channel (the final nn.Conv2d(32,1), latice/model.py:148):
@@ -74,7 +77,8 @@ int ebsdvae_conv3x3_cout1_dgrad(const float* g, const float* w, float* gin, int 
  * Partial dW[co][ci][tap] and db[co] over pixel slices; then ebsdvae_wgrad_reduce sums
  * the slices in fixed order into the parameter-gradient layout of `kind` (0 conv,
  * 1 convT).  Replaces autograd's convolution_backward weight/bias outputs.
- * gy is the conv-output gradient (NHWC, cout channels); src/act as in the forward. */
+ * gy is the conv-output gradient (NHWC, cout channels); src/act as in the forward, except
+ * that max-pool-fed layers pass their materialised pooled activation as RAW. */
 int ebsdvae_conv3x3_wgrad_slices(int B, int H, int W, int cin, int cout);
 int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, int src_mode,
                           const float* gy, float* wpart, float* bpart, int B, int H, int W,

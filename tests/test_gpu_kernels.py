@@ -72,9 +72,15 @@ def test_conv3x3_fwd_and_in_stats(cuda, cin, cout, H, mode):
     w = rng.standard_normal((cout, cin, 3, 3)) / np.sqrt(9 * cin)
     b = rng.standard_normal(cout) * 0.1
     layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
-    y, stt = E.conv_forward(dev(s), dev(st) if mode in (1, 2, 4) else None, layer, dev(w), dev(b), B)
-    ref = O.conv3x3(act_oracle(s, mean, rstd, mode), w, b)
+    keep = cin > 1
+    out = E.conv_forward(dev(s), dev(st) if mode in (1, 2, 4) else None, layer, dev(w), dev(b), B,
+                         keep_act=keep)
+    y, stt = out[0], out[1]
+    a_ref = act_oracle(s, mean, rstd, mode)
+    ref = O.conv3x3(a_ref, w, b)
     assert O.rel_err(host(y), ref) < TOL
+    if keep:   # the materialised conv input (used by pool-fed layers' wgrad)
+        assert O.rel_err(host(out[2]), a_ref) < 1e-6
     _, rm, rr = O.instance_norm(ref)
     got = host(stt)
     assert O.rel_err(got[..., 0], rm[:, 0, 0, :]) < 1e-5
@@ -112,7 +118,15 @@ def test_conv_wgrad_matches_oracle(cuda, cin, cout, H, mode, kind):
     wshape = (cout, cin, 3, 3) if kind == 0 else (cin, cout, 3, 3)
     dw = torch.empty(wshape, device="cuda")
     db = torch.empty(cout, device="cuda")
-    E.conv_wgrad(dev(s), dev(st) if mode in (1, 2, 4) else None, mode, dev(gy), cin, cout, kind, dw, db)
+    if mode == E.ACT_NORM_POOL:
+        # pool-fed layers: the forward conv materialises the pooled activation, the wgrad
+        # reads it RAW
+        layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
+        wdummy = dev(np.zeros((cout, cin, 3, 3)))
+        _, _, act = E.conv_forward(dev(s), dev(st), layer, wdummy, dev(np.zeros(cout)), B, keep_act=True)
+        E.conv_wgrad(act, None, E.ACT_RAW, dev(gy), cin, cout, kind, dw, db)
+    else:
+        E.conv_wgrad(dev(s), dev(st) if mode in (1, 2, 4) else None, mode, dev(gy), cin, cout, kind, dw, db)
     a = act_oracle(s, mean, rstd, mode)
     rw, rb = O.conv3x3_wgrad(a, gy.reshape(B, H, H, cout))
     if kind == 1:
