@@ -26,7 +26,7 @@ constexpr int WG_PT = 128;   // pixels per tile
 constexpr int WG_AS = 48;    // activation halo channel stride (32 + 16)
 
 struct WgGeom {
-  int TH, TW, NI, ntx, nty, tiles, slices, tps;
+  int TH, TW, NI, ntx, nty, tiles, slices, tps, lTW, ltpx;
 };
 
 static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
@@ -42,13 +42,16 @@ static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
   if (W % g->TW || H % g->TH) return false;
   if (g->NI * (g->TH + 2) * (g->TW + 2) > 224) return false;   // KH = 7 halo items / thread
   g->ntx = W / g->TW;
+  g->lTW = __builtin_ctz(g->TW);
+  g->ltpx = __builtin_ctz(g->TH * g->TW);
+  if ((1 << g->lTW) != g->TW || (1 << g->ltpx) != g->TH * g->TW) return false;
   g->nty = H / g->TH;
   const long imgs = (B + g->NI - 1) / g->NI;
   g->tiles = (int)(imgs * g->ntx * g->nty);
   // aim for ~2048 blocks (slices x co tiles x ci tiles), >= 4 tiles per slice
   const int co_t = cout == 1 ? 1 : (cout == 32 ? 1 : cout / 64);
   const int ci_t = cin == 1 ? 1 : (cout == 1 ? 1 : cin / 32);
-  const int want = 2048 / (co_t * ci_t);
+  const int want = 1024 / (co_t * ci_t);
   int tps = 4;
   while ((g->tiles + tps - 1) / tps > (want > 1 ? want : 1)) tps *= 2;
   g->tps = tps;
@@ -115,8 +118,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(
 #pragma unroll
     for (int k = 0; k < KG; ++k) {
       const int px = (tid + 256 * k) / (CO_T / 4);
-      const int img = px / tpx, rem = px - img * tpx;
-      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int img = px >> g.ltpx, rem = px & (tpx - 1);
+      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
       const int gb = b0 + img;
       if (gb < B) rg[k] = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + qg * 4);
     }
@@ -184,8 +187,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(
 #pragma unroll 2
     for (int s = wk; s < WG_PT / 4; s += KSPLIT) {
       const int px = 4 * s + kq;
-      const int img = px / tpx, rem = px - img * tpx;
-      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int img = px >> g.ltpx, rem = px & (tpx - 1);
+      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
       const int hb = ((img * HP + r) * WP + c) * WG_AS + wci * 16 + l16;
       const float a0 = lg[px * GS + wco * 32 + l16];
       const float a1 = lg[px * GS + wco * 32 + 16 + l16];
@@ -262,8 +265,8 @@ __global__ __launch_bounds__(128) void wgrad_cin1_kernel(
     __syncthreads();
     for (int i = tid; i < WG_PT * 8; i += 128) {
       const int px = i >> 3, q = i & 7;
-      const int img = px / tpx, rem = px - img * tpx;
-      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int img = px >> g.ltpx, rem = px & (tpx - 1);
+      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
       const int gb = b0 + img;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (gb < B) v = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + q * 4);
@@ -286,8 +289,8 @@ __global__ __launch_bounds__(128) void wgrad_cin1_kernel(
     }
     for (int s = 0; s < WG_PT / 4; ++s) {
       const int px = 4 * s + kq;
-      const int img = px / tpx, rem = px - img * tpx;
-      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int img = px >> g.ltpx, rem = px & (tpx - 1);
+      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
       const float a = lg[px * GS + wave * 16 + l16];
       const float bv = l16 < 9 ? la[(img * HP + r + tkh) * WP + c + tkw] : 0.f;
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
@@ -330,8 +333,8 @@ __global__ __launch_bounds__(128) void wgrad_cout1_kernel(
     __syncthreads();
     for (int i = tid; i < WG_PT * 8; i += 128) {
       const int px = i >> 3, q = i & 7;
-      const int img = px / tpx, rem = px - img * tpx;
-      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int img = px >> g.ltpx, rem = px & (tpx - 1);
+      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
       const int gb = b0 + img;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (gb < B) v = load_act4(src, sstats, smode, gb, y0 + r, x0 + c, q * 4, H, W, Cin);
@@ -355,8 +358,8 @@ __global__ __launch_bounds__(128) void wgrad_cout1_kernel(
     }
     for (int s = 0; s < WG_PT / 4; ++s) {
       const int px = 4 * s + kq;
-      const int img = px / tpx, rem = px - img * tpx;
-      const int r = rem / g.TW, c = rem - r * g.TW;
+      const int img = px >> g.ltpx, rem = px & (tpx - 1);
+      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
       // g[q - d(tap)] with d(tap) = (kh-1, kw-1): halo coordinate (r+1-(kh-1), c+1-(kw-1))
       const float a = l16 < 9 ? lgh[(img * HP + r + 2 - tkh) * WP + c + 2 - tkw] : 0.f;
       const float bv = la[px * AS + wave * 16 + l16];
@@ -417,10 +420,10 @@ __global__ void wgrad_reduce2_kernel(const double* __restrict__ work, int G, flo
 
 static int reduce_groups(int slices, int cin, int cout) {
   const int E = 9 * cin * cout + cout;
-  int G = 262144 / E;
-  if (G < 1) G = 1;
-  if (G > slices) G = slices;
+  int G = 524288 / E;
+  if (G < 8) G = 8;
   if (G > 64) G = 64;
+  if (G > slices) G = slices;
   return G;
 }
 

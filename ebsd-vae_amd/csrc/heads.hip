@@ -132,38 +132,27 @@ __global__ __launch_bounds__(256) void heads_wgrad_kernel(
     const float* __restrict__ flat, const float* __restrict__ z, const float* __restrict__ gs,
     float* __restrict__ gwmu, float* __restrict__ gbmu, float* __restrict__ gwlv,
     float* __restrict__ gblv, float* __restrict__ gw2, float* __restrict__ gb2, int B, int F, int L) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  // thread (j, e): e fastest (coalesced flat / g_out rows), j = latent index
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int G = 2 * L + F;
-  if (e < F) {
-    float am[MAXL], al[MAXL], a2[MAXL];
-#pragma unroll
-    for (int j = 0; j < MAXL; ++j) { am[j] = 0.f; al[j] = 0.f; a2[j] = 0.f; }
-    float ab = 0.f;
+  if (idx < F * L) {
+    const int j = idx / F, e = idx - j * F;
+    float am = 0.f, al = 0.f, a2 = 0.f, ab = 0.f;
     for (int b = 0; b < B; ++b) {
       const float fv = flat[(size_t)b * F + e];
       const float go = gs[(size_t)b * G + 2 * L + e];
       const float* gb = gs + (size_t)b * G;
-      const float* zb = z + (size_t)b * L;
+      am = fmaf(gb[j], fv, am);
+      al = fmaf(gb[L + j], fv, al);
+      a2 = fmaf(go, z[(size_t)b * L + j], a2);
       ab += go;
-#pragma unroll
-      for (int j = 0; j < MAXL; ++j) {
-        if (j < L) {
-          am[j] = fmaf(gb[j], fv, am[j]);
-          al[j] = fmaf(gb[L + j], fv, al[j]);
-          a2[j] = fmaf(go, zb[j], a2[j]);
-        }
-      }
     }
-#pragma unroll
-    for (int j = 0; j < MAXL; ++j) {
-      if (j < L) {
-        gwmu[(size_t)j * F + e] = am[j];
-        gwlv[(size_t)j * F + e] = al[j];
-        gw2[(size_t)e * L + j] = a2[j];
-      }
-    }
-    gb2[e] = ab;
-  } else if (e < F + L) {
+    gwmu[(size_t)j * F + e] = am;
+    gwlv[(size_t)j * F + e] = al;
+    gw2[(size_t)e * L + j] = a2;
+    if (j == 0) gb2[e] = ab;
+  } else if (idx < F * L + L) {
+    const int e = idx - F * L + F;
     const int j = e - F;
     float sm = 0.f, sl = 0.f;
     for (int b = 0; b < B; ++b) {
@@ -315,7 +304,7 @@ extern "C" int ebsdvae_heads_wgrad(const float* flat, const float* z, const floa
   EV_REQUIRE(flat && z && gs && gw_mu && gb_mu && gw_lv && gb_lv && gw_l2 && gb_l2,
              "heads_wgrad: null pointer");
   EV_REQUIRE(L > 0 && L <= MAXL, "heads_wgrad: bad L");
-  const int n = F + L;
+  const int n = F * L + L;
   hipLaunchKernelGGL(heads_wgrad_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      flat, z, gs, gw_mu, gb_mu, gw_lv, gb_lv, gw_l2, gb_l2, B, F, L);
   return evh::check_launch("heads_wgrad");

@@ -20,24 +20,44 @@ enum PMode : int { P_ID = 0, P_POOL = 1, P_UP = 2 };
 
 EV_DEVINL float slope(float xh) { return xh > 0.f ? 1.f : kSlope; }
 
-__global__ void in_stats_finalize_kernel(const float2* __restrict__ part, float2* __restrict__ st,
-                                         int B, int C, int T, float n) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= B * C) return;
-  const int b = e / C, c = e - b * C;
+// One workgroup per pattern b: thread (c = tid % C, j = tid / C) folds tiles j, j+J, ... of
+// channel c (coalesced over c), then lane j == 0 folds the J partial results in order.
+// All tiles hold n elements, so the Chan merge reduces to: mean = avg(mean_t),
+// M2 = sum(M2_t) + n * sum((mean_t - mean)^2).
+__global__ __launch_bounds__(256) void in_stats_finalize_kernel(const float2* __restrict__ part,
+                                                                float2* __restrict__ st, int C,
+                                                                int T, float n) {
+  __shared__ float sm[3][256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int J = 256 / C;
+  const int c = tid % C, j = tid / C;
   const float2* p = part + (size_t)b * T * C + c;
   float m = 0.f;
-  for (int t = 0; t < T; ++t) m += p[(size_t)t * C].x;
-  m /= (float)T;
+  int cnt = 0;
+  for (int t = j; t < T; t += J) { m += p[(size_t)t * C].x; ++cnt; }
+  sm[0][tid] = m;
+  sm[1][tid] = (float)cnt;
+  __syncthreads();
+  float mean = 0.f;
+  for (int k = 0; k < J; ++k) mean += sm[0][k * C + c];
+  mean /= (float)T;
   float m2 = 0.f, dm = 0.f;
-  for (int t = 0; t < T; ++t) {
+  for (int t = j; t < T; t += J) {
     const float2 v = p[(size_t)t * C];
     m2 += v.y;
-    const float d = v.x - m;
+    const float d = v.x - mean;
     dm = fmaf(d, d, dm);
   }
-  const float var = (m2 + n * dm) / (n * (float)T);
-  st[e] = make_float2(m, 1.0f / sqrtf(var + kInEps));
+  __syncthreads();
+  sm[0][tid] = m2;
+  sm[2][tid] = dm;
+  __syncthreads();
+  if (j == 0) {
+    float a = 0.f, q = 0.f;
+    for (int k = 0; k < J; ++k) { a += sm[0][k * C + c]; q += sm[2][k * C + c]; }
+    const float var = (a + n * q) / (n * (float)T);
+    st[(size_t)b * C + c] = make_float2(mean, 1.0f / sqrtf(var + kInEps));
+  }
 }
 
 __global__ void act_apply_kernel(const float* __restrict__ src, const float2* __restrict__ st,
@@ -229,6 +249,182 @@ __global__ void in_bwd_finalize_kernel(const double2* __restrict__ part, float2*
   bst[e] = make_float2((float)(s1 * inv_hw), (float)(s2 * inv_hw));
 }
 
+// ------------------------------------------------------------------ network-end fusions
+// (C == 32 planes, row-band tiles as in_bwd_kernel; thread = (channel group cg, pixel row pr))
+//
+// FINAL: the block feeding the last conv nn.Conv2d(32,1) (latice/model.py:147-148).  Its
+// output gradient g_a[q][c] = sum_tap g1[q - d(tap)] * w14[c][tap] is recomputed from the
+// 1-channel logit gradient g1 (never materialised), and the reduce pass also accumulates
+// that conv's weight/bias gradient dW14[c][tap] = sum_q g1[q - d(tap)] * a[q][c].
+// FIRST: the block of the first conv nn.Conv2d(1,32) (latice/model.py:110).  Its apply pass
+// accumulates dW0[c][tap] = sum_p gy[p][c] * x[p + d(tap)] and db0 directly, so gy is never
+// written (the input x needs no gradient).
+// Partials are per (b, tile) "slice" in the [slice][tap][co][ci] layout of
+// ebsdvae_wgrad_reduce.
+enum EdgeFuse : int { FUSE_FINAL = 1, FUSE_FIRST = 2 };
+
+EV_DEVINL void wave_fold8(float& v) {  // sum over the 8 pixel rows of a wave (lanes l, l^8, ...)
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+}
+
+template <int FUSE, bool APPLY>
+__global__ __launch_bounds__(256) void in_bwd_edge_kernel(
+    const float* __restrict__ gsrc, const float* __restrict__ w14, const float* __restrict__ y,
+    const float2* __restrict__ st, const float2* __restrict__ bst, const float* __restrict__ x,
+    double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart,
+    float* __restrict__ gy, int H, int W, int T) {
+  constexpr int C = 32, CG = 8, NPR = 32;
+  __shared__ double red[2][4][256];
+  __shared__ float wred[4][CG][37];
+  const int tile = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cg = tid % CG, pr = tid / CG;
+  const int c = cg * 4;
+  const int rows = H / T;
+  const float2* sp = st + (size_t)b * C + c;
+  float mean[4], rstd[4], m1[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { const float2 v = sp[k]; mean[k] = v.x; rstd[k] = v.y; }
+  if (APPLY) {
+    const float2* bp = bst + (size_t)b * C + c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { m1[k] = bp[k].x; m2[k] = bp[k].y; }
+  }
+  float wv[4][9];
+  if (FUSE == FUSE_FINAL) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wv[k][t] = w14[(c + k) * 9 + t];
+  }
+  double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+  float wacc[4][9];
+  float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wacc[k][t] = 0.f;
+  const float* yb = y + (size_t)b * H * W * C;
+  const float* gb1 = gsrc + (size_t)b * H * W;   // FINAL: g1 (1 channel)
+  const float* xb = (FUSE == FUSE_FIRST) ? x + (size_t)b * H * W : nullptr;
+  const int p0 = tile * rows * W, p1 = p0 + rows * W;
+  for (int p = p0 + pr; p < p1; p += NPR) {
+    const int h = p / W, w = p - h * W;
+    float nb[9];   // FINAL: g1[q - d(tap)] ; FIRST: x[p + d(tap)]
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t % 3;
+      const int hh = (FUSE == FUSE_FINAL) ? h + 1 - kh : h + kh - 1;
+      const int ww = (FUSE == FUSE_FINAL) ? w + 1 - kw : w + kw - 1;
+      const bool ok = hh >= 0 && hh < H && ww >= 0 && ww < W;
+      nb[t] = ok ? ((FUSE == FUSE_FINAL) ? gb1[hh * W + ww] : xb[hh * W + ww]) : 0.f;
+    }
+    float ga[4];
+    if (FUSE == FUSE_FINAL) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) s = fmaf(nb[t], wv[k][t], s);
+        ga[k] = s;
+      }
+      if (!APPLY && cg == 0) bacc[0] += nb[4];   // g1[p] itself (centre tap): db14
+    } else {
+      const float4 g4 = ld4(gsrc + ((size_t)b * H * W + p) * C + c);
+      ga[0] = g4.x; ga[1] = g4.y; ga[2] = g4.z; ga[3] = g4.w;
+    }
+    const float4 y4 = ld4(yb + (size_t)p * C + c);
+    const float yy[4] = {y4.x, y4.y, y4.z, y4.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float xh = (yy[k] - mean[k]) * rstd[k];
+      const float gx = ga[k] * slope(xh);
+      if (!APPLY) {
+        a1[k] += (double)gx;
+        a2[k] = fma((double)gx, (double)xh, a2[k]);
+        if (FUSE == FUSE_FINAL) {
+          const float av = lrelu(xh);
+#pragma unroll
+          for (int t = 0; t < 9; ++t) wacc[k][t] = fmaf(nb[t], av, wacc[k][t]);
+        }
+      } else {
+        o[k] = rstd[k] * (gx - m1[k] - xh * m2[k]);
+        if (FUSE == FUSE_FIRST) {
+          bacc[k] += o[k];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) wacc[k][t] = fmaf(o[k], nb[t], wacc[k][t]);
+        }
+      }
+    }
+    if (APPLY && FUSE == FUSE_FINAL)
+      st4(gy + ((size_t)b * H * W + p) * C + c, make_float4(o[0], o[1], o[2], o[3]));
+  }
+  const int slice = b * T + tile;
+  if (!APPLY) {   // InstanceNorm-backward plane partials (double, fixed order)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { red[0][k][tid] = a1[k]; red[1][k][tid] = a2[k]; }
+    __syncthreads();
+    if (tid < CG) {
+      double u[4], v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { u[k] = red[0][k][tid]; v[k] = red[1][k][tid]; }
+      for (int r = 1; r < NPR; ++r) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { u[k] += red[0][k][r * CG + tid]; v[k] += red[1][k][r * CG + tid]; }
+      }
+      double2* op = part + (size_t)slice * C + c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) op[k] = make_double2(u[k], v[k]);
+    }
+  }
+  if ((FUSE == FUSE_FINAL && !APPLY) || (FUSE == FUSE_FIRST && APPLY)) {
+    // fold the 36 weight partials (+ bias) of the block: in-wave over its 8 pixel rows,
+    // then across the 4 waves in order
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        float v = wacc[k][t];
+        wave_fold8(v);
+        if (lane < CG) wred[wave][lane][k * 9 + t] = v;
+      }
+      float v = bacc[k];
+      wave_fold8(v);
+      // bias: FINAL keeps one scalar (k == 0, cg == 0 lane); FIRST keeps 4 per channel group
+      if (lane < CG) {
+        if (FUSE == FUSE_FINAL && k == 0) wred[wave][lane][36] = v;
+        if (FUSE == FUSE_FIRST) bacc[k] = v;
+      }
+    }
+    __syncthreads();
+    // FINAL: Cout = 1, Cin = 32 -> [slice][tap][0][ci];  FIRST: Cout = 32, Cin = 1 ->
+    // [slice][tap][co][0]; both are offset t * 32 + channel
+    for (int i = tid; i < CG * 36; i += 256) {
+      const int g = i / 36, e = i % 36;   // channel group, (k, tap)
+      const float s = wred[0][g][e] + wred[1][g][e] + wred[2][g][e] + wred[3][g][e];
+      const int k = e / 9, t = e % 9;
+      wpart[((size_t)slice * 9 + t) * 32 + g * 4 + k] = s;
+    }
+    if (FUSE == FUSE_FINAL && tid == 0)
+      bpart[slice] = wred[0][0][36] + wred[1][0][36] + wred[2][0][36] + wred[3][0][36];
+    if (FUSE == FUSE_FIRST) {
+      __syncthreads();
+      if (lane < CG) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wred[wave][lane][k] = bacc[k];
+      }
+      __syncthreads();
+      if (tid < C) {
+        const int g = tid / 4, k = tid % 4;
+        bpart[(size_t)slice * 32 + tid] = wred[0][g][k] + wred[1][g][k] + wred[2][g][k] + wred[3][g][k];
+      }
+    }
+  }
+}
+
 static int grid_for(size_t n4) {
   size_t g = (n4 + 255) / 256;
   if (g > 8192) g = 8192;
@@ -242,11 +438,10 @@ using namespace ev;
 
 extern "C" int ebsdvae_in_stats_finalize(const float* part, float* stats, int B, int C, int tiles,
                                          int n_per_tile, ebsdvae_stream_t stream) {
-  EV_REQUIRE(part && stats && B > 0 && C > 0 && tiles > 0, "in_stats_finalize: bad args");
-  const int n = B * C;
-  hipLaunchKernelGGL(in_stats_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, (const float2*)part, (float2*)stats, B, C, tiles,
-                     (float)n_per_tile);
+  EV_REQUIRE(part && stats && B > 0 && C > 0 && tiles > 0 && C <= 256 && (256 % C) == 0,
+             "in_stats_finalize: bad args (C=%d)", C);
+  hipLaunchKernelGGL(in_stats_finalize_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream,
+                     (const float2*)part, (float2*)stats, C, tiles, (float)n_per_tile);
   return evh::check_launch("in_stats_finalize");
 }
 
@@ -309,4 +504,45 @@ extern "C" int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* 
                      pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy, H,
                      W, C, T);
   return evh::check_launch("in_bwd_apply");
+}
+
+// ------------------------------------------------------------------ network-end fusions (ABI)
+extern "C" int ebsdvae_in_bwd_final_reduce(const float* g1, const float* w14, const float* y,
+                                           const float* stats, double* part, float* wpart,
+                                           float* bpart, int B, int H, int W, int C,
+                                           ebsdvae_stream_t stream) {
+  EV_REQUIRE(g1 && w14 && y && stats && part && wpart && bpart && C == 32,
+             "in_bwd_final_reduce: bad args (C must be 32)");
+  const int T = in_bwd_tiles_host(H, W);
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, false>), dim3(T, B), dim3(256), 0,
+                     (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)nullptr,
+                     (const float*)nullptr, (double2*)part, wpart, bpart, (float*)nullptr, H, W, T);
+  return evh::check_launch("in_bwd_final_reduce");
+}
+
+extern "C" int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, const float* y,
+                                          const float* stats, const float* bstats, float* gy,
+                                          int B, int H, int W, int C, ebsdvae_stream_t stream) {
+  EV_REQUIRE(g1 && w14 && y && stats && bstats && gy && C == 32,
+             "in_bwd_final_apply: bad args (C must be 32)");
+  const int T = in_bwd_tiles_host(H, W);
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), 0,
+                     (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)bstats,
+                     (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
+                     H, W, T);
+  return evh::check_launch("in_bwd_final_apply");
+}
+
+extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float* y,
+                                                const float* stats, const float* bstats,
+                                                const float* x, float* wpart, float* bpart, int B,
+                                                int H, int W, int C, ebsdvae_stream_t stream) {
+  EV_REQUIRE(gnext && y && stats && bstats && x && wpart && bpart && C == 32,
+             "in_bwd_first_apply_wgrad: bad args (C must be 32)");
+  const int T = in_bwd_tiles_host(H, W);
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true>), dim3(T, B), dim3(256), 0,
+                     (hipStream_t)stream, gnext, (const float*)nullptr, y, (const float2*)stats,
+                     (const float2*)bstats, x, (double2*)nullptr, wpart, bpart, (float*)nullptr, H, W,
+                     T);
+  return evh::check_launch("in_bwd_first_apply_wgrad");
 }

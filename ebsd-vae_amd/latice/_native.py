@@ -41,6 +41,9 @@ SIGNATURES = {
     "ebsdvae_in_bwd_finalize": [P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_apply": [P, I, P, P, P, P, I, I, I, I, P],
     "ebsdvae_upsample2_bwd": [P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_final_reduce": [P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_final_apply": [P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_first_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_wgrad": [P, P, P, P, P, P, P, P, P, I, I, I, P],

@@ -192,6 +192,55 @@ def in_backward(gnext, pmode, y, st):
     return gy
 
 
+def _in_bwd_stats(B, C, T, HW, part, like):
+    bst = _empty(B, C, 2, like=like)
+    N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, T, HW, N.stream())
+    return bst
+
+
+def _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db):
+    nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
+    work = torch.empty(nbytes // 8, dtype=torch.float64, device=wpart.device)
+    N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db), cin, cout,
+           kind, work.data_ptr(), N.stream())
+
+
+def in_backward_final(g1, w14, y, st, dw14, db14):
+    """Backward of the last conv block + the final conv(32->1) (latice/model.py:147-148):
+    returns gy of the last block and writes the final conv's dW/db."""
+    B, H, W, C = y.shape
+    T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
+    S_ = B * T
+    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
+    wpart = _empty(S_, 9, 1, C, like=y)
+    bpart = _empty(S_, 1, like=y)
+    N.call("ebsdvae_in_bwd_final_reduce", N.ptr(g1), N.ptr(w14), N.ptr(y), N.ptr(st),
+           part.data_ptr(), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
+    bst = _in_bwd_stats(B, C, T, H * W, part, y)
+    gy = torch.empty_like(y)
+    N.call("ebsdvae_in_bwd_final_apply", N.ptr(g1), N.ptr(w14), N.ptr(y), N.ptr(st), N.ptr(bst),
+           N.ptr(gy), B, H, W, C, N.stream())
+    _reduce_slices(wpart, bpart, S_, C, 1, KIND_CONV, dw14, db14)
+    return gy
+
+
+def in_backward_first(gnext, y, st, x, dw0, db0):
+    """Backward of the first conv block (latice/model.py:110): writes dW/db of the 1->32
+    conv directly from the InstanceNorm-backward apply pass (gy is never materialised)."""
+    B, H, W, C = y.shape
+    T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
+    S_ = B * T
+    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
+    N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), P_ID, N.ptr(y), N.ptr(st), part.data_ptr(),
+           B, H, W, C, N.stream())
+    bst = _in_bwd_stats(B, C, T, H * W, part, y)
+    wpart = _empty(S_, 9, C, 1, like=y)
+    bpart = _empty(S_, C, like=y)
+    N.call("ebsdvae_in_bwd_first_apply_wgrad", N.ptr(gnext), N.ptr(y), N.ptr(st), N.ptr(bst),
+           N.ptr(x), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
+    _reduce_slices(wpart, bpart, S_, 1, C, KIND_CONV, dw0, db0)
+
+
 def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
     B, H, W, _ = gy.shape if gy.dim() == 4 else (*gy.shape, 1)
     S_ = N.call("ebsdvae_conv3x3_wgrad_slices", B, H, W, cin, cout)
@@ -255,6 +304,14 @@ def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=Fa
     for i in reversed(range(len(plan.enc))):
         L = plan.enc[i]
         y, st = saved[L.name]
+        if i == 0 and not need_gx:
+            # first conv's weight gradient fused into its block's InstanceNorm backward
+            wn, bn = L.name + ".weight", L.name + ".bias"
+            dw = _grad_buf(grads, wn, params[wn])
+            db = _grad_buf(grads, bn, params[bn])
+            in_backward_first(g_next, y, st, x, dw, db)
+            out[wn], out[bn] = dw, db
+            break
         gy = in_backward(g_next, L.pmode, y, st)
         mode = L.src_mode
         if i == 0:
@@ -341,15 +398,15 @@ def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None):
     dw = _grad_buf(grads, wn, params[wn])
     db = _grad_buf(grads, bn, params[bn])
     g1 = g_xhat.reshape(B, S, S)
-    conv_wgrad(y13, st13, ACT_NORM, g1, p, 1, KIND_CONV, dw, db)
+    # last conv fused into the last block's InstanceNorm backward: its input gradient is
+    # recomputed from g1 on the fly, its weight gradient accumulated in the reduce pass
+    gy_last = in_backward_final(g1, params[wn], y13, st13, dw, db)
     out[wn], out[bn] = dw, db
-    g_next = _empty(B, S, S, p, like=g_xhat)
-    N.call("ebsdvae_conv3x3_cout1_dgrad", N.ptr(g1), N.ptr(params[wn]), N.ptr(g_next), B, S, S, p,
-           N.stream())
+    g_next = None
     for i in reversed(range(len(plan.dec))):
         L = plan.dec[i]
         y, st = saved[L.name]
-        gy = in_backward(g_next, L.pmode, y, st)
+        gy = gy_last if i == len(plan.dec) - 1 else in_backward(g_next, L.pmode, y, st)
         wn, bn = L.name + ".weight", L.name + ".bias"
         src, sst = (saved["__dec_in__"], None) if i == 0 else saved[plan.dec[i - 1].name]
         dw = _grad_buf(grads, wn, params[wn])

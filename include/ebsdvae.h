@@ -113,6 +113,25 @@ int ebsdvae_in_bwd_finalize(const double* part, float* bstats, int B, int C, int
 int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* y, const float* stats,
                          const float* bstats, float* gy, int B, int H, int W, int C,
                          ebsdvae_stream_t stream);
+/* Network-end fusions (C == 32; slices = B * ebsdvae_in_bwd_tiles(H,W,C) partials for
+ * ebsdvae_wgrad_reduce):
+ *  final_*: the block feeding the last conv (latice/model.py:147-148).  Its output gradient
+ *    sum_tap g1[q-d(tap)] * w14[c][tap] is recomputed from the 1-channel logit gradient g1
+ *    (never materialised); the reduce pass also emits that conv's dW (cin=32, cout=1) and
+ *    db partials.
+ *  first_apply_wgrad: the apply pass of the first block (latice/model.py:110) that
+ *    accumulates the first conv's dW (cin=1, cout=32) and db partials against the input x
+ *    instead of writing gy (x needs no gradient). */
+int ebsdvae_in_bwd_final_reduce(const float* g1, const float* w14, const float* y,
+                                const float* stats, double* part, float* wpart, float* bpart,
+                                int B, int H, int W, int C, ebsdvae_stream_t stream);
+int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, const float* y,
+                               const float* stats, const float* bstats, float* gy, int B, int H,
+                               int W, int C, ebsdvae_stream_t stream);
+int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float* y, const float* stats,
+                                     const float* bstats, const float* x, float* wpart,
+                                     float* bpart, int B, int H, int W, int C,
+                                     ebsdvae_stream_t stream);
 /* gradient of nearest x2 upsampling: out[b,h,w,c] = sum of the 2x2 block of g (at 2H) */
 int ebsdvae_upsample2_bwd(const float* g, float* out, int B, int H, int W, int C,
                           ebsdvae_stream_t stream);

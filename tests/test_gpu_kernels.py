@@ -303,3 +303,42 @@ def test_fused_adam_matches_torch_adam(cuda, amsgrad):
         ob.step()
     torch.cuda.synchronize()
     assert torch.allclose(pa, pb, rtol=1e-6, atol=1e-7)
+
+
+def test_fused_final_conv_backward(cuda):
+    """Last block + final conv(32->1): gy of the block and dW/db of the final conv from the
+    1-channel logit gradient, without materialising the block's output gradient."""
+    rng = np.random.default_rng(21)
+    B, H, C = 2, 64, 32
+    y = rng.standard_normal((B, H, H, C)) * 1.7 + 0.2
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    w14 = rng.standard_normal((1, C, 3, 3)) * 0.2
+    g1 = rng.standard_normal((B, H, H))
+    dw = torch.empty(1, C, 3, 3, device="cuda")
+    db = torch.empty(1, device="cuda")
+    gy = E.in_backward_final(dev(g1), dev(w14), dev(y), dev(st), dw, db)
+    ga = O.conv3x3_dgrad(g1[..., None], w14)
+    ref_gy = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
+    rw, rb = O.conv3x3_wgrad(O.lrelu(xh), g1[..., None])
+    assert O.rel_err(host(gy), ref_gy) < 1e-4
+    assert O.rel_err(host(dw), rw) < 5e-5
+    assert O.rel_err(host(db), rb) < 5e-5
+
+
+def test_fused_first_conv_weight_grad(cuda):
+    """First block: dW/db of the conv(1->32) straight from the InstanceNorm-backward pass."""
+    rng = np.random.default_rng(22)
+    B, H, C = 2, 64, 32
+    y = rng.standard_normal((B, H, H, C)) * 1.3 - 0.4
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    gn = rng.standard_normal((B, H, H, C))
+    x = np.floor(rng.random((B, H, H, 1)) * 255) / 255
+    dw = torch.empty(C, 1, 3, 3, device="cuda")
+    db = torch.empty(C, device="cuda")
+    E.in_backward_first(dev(gn), dev(y), dev(st), dev(x), dw, db)
+    gy = O.instance_norm_bwd(gn * O.lrelu_slope(xh), xh, rstd)
+    rw, rb = O.conv3x3_wgrad(x, gy)
+    assert O.rel_err(host(dw), rw) < 1e-4
+    assert np.abs(host(db) - rb).max() < 1e-4 * max(1.0, np.abs(rb).max())
