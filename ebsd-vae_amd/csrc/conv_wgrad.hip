@@ -49,7 +49,8 @@ static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
   const long imgs = (B + g->NI - 1) / g->NI;
   g->tiles = (int)(imgs * g->ntx * g->nty);
   // aim for ~2048 blocks (slices x co tiles x ci tiles), >= 4 tiles per slice
-  const int co_t = cout == 1 ? 1 : (cout == 32 ? 1 : cout / 64);
+  // 8x8 maps (two-image tiles) use 32-wide co tiles: the 64-wide variant exceeds 256 VGPRs
+  const int co_t = cout == 1 ? 1 : (cout == 32 || g->TW == 8 ? cout / 32 : cout / 64);
   const int ci_t = cin == 1 ? 1 : (cout == 1 ? 1 : cin / 32);
   const int want = 1024 / (co_t * ci_t);
   int tps = 4;
@@ -68,104 +69,132 @@ EV_DEVINL void tile_origin(int t, const WgGeom& g, int& b0, int& y0, int& x0) {
 }
 
 // ------------------------------------------------------------------ generic (cin % 32 == 0)
+// Tile geometry is a compile-time function of TW (the tile width, min(W, 32)): 128 pixels
+// as 4x32, 8x16 or 2 images of 8x8.  With it, and the k-step loop fully unrolled, every
+// LDS operand address is a per-lane base register plus an immediate offset.
+template <int TW>
+struct WgTile {
+  static constexpr int TH = TW == 32 ? 4 : 8;
+  static constexpr int NI = TW == 8 ? 2 : 1;
+  static constexpr int HP = TH + 2, WP = TW + 2;
+  static constexpr int HALO = NI * HP * WP;   // 204 / 180 / 200 pixels
+  static constexpr int IPX = TH * TW;         // pixels per image in the tile
+  static_assert(NI * IPX == WG_PT, "128-pixel tiles");
+  static_assert(HALO * 8 <= 7 * 256, "7 halo float4 items per thread");
+};
+
 // Software-pipelined over the slice's pixel tiles: the NEXT tile's gy rows and raw
 // activation halo (+ its InstanceNorm stats) are loaded into registers while the MFMAs of
 // the current tile run; the transform (InstanceNorm + LeakyReLU [+ upsample]) is applied
-// when they are written to LDS.  MODE is never NORM_POOL here: pool-fed layers pass the
-// pooled activation that their forward conv materialised (RAW).
-template <int NWCO, int KSPLIT, int MODE>
-__global__ __launch_bounds__(256) void wgrad_kernel(
+// when they are written to LDS.  The bias gradient is summed from the same gy registers.
+// MODE is never NORM_POOL here: pool-fed layers pass the pooled activation that their
+// forward conv materialised (RAW).
+template <int NWCO, int KSPLIT, int MODE, int TW>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats,
     const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
     int H, int W, int Cin, int Cout, WgGeom g) {
+  using T = WgTile<TW>;
   constexpr int CO_T = NWCO * 32;
   constexpr int GS = CO_T + 16;
-  constexpr int KG = CO_T / 8;    // gy float4 items per thread per tile
-  constexpr int KH = 7;           // halo float4 items per thread per tile (upper bound)
+  constexpr int QG = CO_T / 4;      // float4 channel groups of a gy pixel
+  constexpr int KG = CO_T / 8;      // gy float4 items per thread per tile
+  constexpr int KH = 7;             // halo float4 items per thread per tile (upper bound)
   constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_UP);
   constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
   static_assert(NWCO * 2 * KSPLIT == 4, "4 waves per block");
   static_assert(MODE != ACT_NORM_POOL, "pool-fed layers use the materialised activation");
+  constexpr int SPR = TW / (4 * KSPLIT);        // k-steps per tile row
+  constexpr int ROW_UNROLL = 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lg = smem;                 // [128][GS]
   float* la = smem + WG_PT * GS;    // [halo px][48]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
   const int slice = blockIdx.x, co0 = blockIdx.y * CO_T, ci0 = blockIdx.z * 32;
-  const int HP = g.TH + 2, WP = g.TW + 2, halo = g.NI * HP * WP;
   const int l16 = lane & 15, kq = lane >> 4;
   const int Hs = UPS ? H / 2 : H, Ws = UPS ? W / 2 : W;
   const int qh = tid & 7;           // this thread's 4-channel group of every halo pixel
-  const int qg = tid % (CO_T / 4);  // this thread's 4-channel group of every gy pixel
+  const int qg = tid % QG;          // this thread's 4-channel group of every gy pixel
+  const bool do_bias = blockIdx.z == 0;
 
   f32x4 acc[2][9];
 #pragma unroll
   for (int f = 0; f < 2; ++f)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  double bsum = 0.0;  // bias partial for co0 + tid (tid < CO_T), ci tile 0 only
+  double bs[4] = {0.0, 0.0, 0.0, 0.0};   // bias partial of channels co0 + 4*qg + 0..3
 
+  const int per_img = g.ntx * g.nty;
   const int t_beg = slice * g.tps;
   const int t_end = min(t_beg + g.tps, g.tiles);
-  const int tpx = g.TH * g.TW;
   float4 rg[KG], rh[KH];
-  float2 st[2][4];
+  float2 st[T::NI][4];
   int cb0 = 0, cy0 = 0, cx0 = 0;   // origin of the tile held in registers
+  auto load_stats = [&](int b0) {
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i) {
+      const int gb = min(b0 + i, B - 1);
+      const float2* sp = sstats + (size_t)gb * Cin + ci0 + qh * 4;
+      st[i][0] = sp[0]; st[i][1] = sp[1]; st[i][2] = sp[2]; st[i][3] = sp[3];
+    }
+  };
   auto issue = [&](int t) {
-    int b0, y0, x0;
-    tile_origin(t, g, b0, y0, x0);
+    const int ib = t / per_img, rr = t - ib * per_img;
+    const int ty = rr / g.ntx;
+    const int b0 = ib * T::NI, y0 = ty * T::TH, x0 = (rr - ty * g.ntx) * TW;
     cb0 = b0; cy0 = y0; cx0 = x0;
 #pragma unroll
     for (int k = 0; k < KG; ++k) {
-      const int px = (tid + 256 * k) / (CO_T / 4);
-      const int img = px >> g.ltpx, rem = px & (tpx - 1);
-      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
+      const int px = (tid + 256 * k) / QG;
+      const int img = px / T::IPX, rem = px % T::IPX;
+      const int r = rem / TW, c = rem % TW;
       const int gb = b0 + img;
-      if (gb < B) rg[k] = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + qg * 4);
+      if (T::NI == 1 || gb < B)
+        rg[k] = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + qg * 4);
     }
 #pragma unroll
     for (int k = 0; k < KH; ++k) {
       const int pix = (tid + 256 * k) >> 3;
-      const int img = pix / (HP * WP), rem = pix - img * (HP * WP);
-      const int hh = rem / WP, ww = rem - hh * WP;
+      const int img = pix / (T::HP * T::WP), rem = pix % (T::HP * T::WP);
+      const int hh = rem / T::WP, ww = rem % T::WP;
       const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
-      if (pix < halo && gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
+      if (pix < T::HALO && gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
         const int sh = UPS ? (gh >> 1) : gh, sw = UPS ? (gw >> 1) : gw;
         rh[k] = ld4(src + (((size_t)gb * Hs + sh) * Ws + sw) * Cin + ci0 + qh * 4);
       }
     }
-    if (NORM) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int gb = min(b0 + i, B - 1);
-        const float2* sp = sstats + (size_t)gb * Cin + ci0 + qh * 4;
-        st[i][0] = sp[0]; st[i][1] = sp[1]; st[i][2] = sp[2]; st[i][3] = sp[3];
-      }
-    }
+    if (NORM && T::NI == 1) load_stats(b0);
   };
   auto store = [&]() {
+    // two-image tiles fetch their stats here (L2-resident) to stay within 256 VGPRs
+    if (NORM && T::NI > 1) load_stats(cb0);
+    float4 tb = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < KG; ++k) {
-      const int px = (tid + 256 * k) / (CO_T / 4);
-      const int img = px / tpx;
+      const int px = (tid + 256 * k) / QG;
       float4 v = rg[k];
-      if (cb0 + img >= B) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (T::NI > 1 && cb0 + px / T::IPX >= B) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      tb.x += v.x; tb.y += v.y; tb.z += v.z; tb.w += v.w;
       st4(lg + px * GS + qg * 4, v);
     }
+    bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
 #pragma unroll
     for (int k = 0; k < KH; ++k) {
       const int pix = (tid + 256 * k) >> 3;
-      if (pix < halo) {
-        const int img = pix / (HP * WP), rem = pix - img * (HP * WP);
-        const int hh = rem / WP, ww = rem - hh * WP;
+      if (pix < T::HALO) {
+        const int img = pix / (T::HP * T::WP), rem = pix % (T::HP * T::WP);
+        const int hh = rem / T::WP, ww = rem % T::WP;
         const int gh = cy0 + hh - 1, gw = cx0 + ww - 1, gb = cb0 + img;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
           v = rh[k];
           if (NORM) {
-            const float2* s4 = st[img > 0 ? 1 : 0];
-            v = make_float4(normact(v.x, s4[0]), normact(v.y, s4[1]), normact(v.z, s4[2]),
-                            normact(v.w, s4[3]));
+            const bool second = T::NI > 1 && img > 0;
+            v = make_float4(normact(v.x, second ? st[T::NI - 1][0] : st[0][0]),
+                            normact(v.y, second ? st[T::NI - 1][1] : st[0][1]),
+                            normact(v.z, second ? st[T::NI - 1][2] : st[0][2]),
+                            normact(v.w, second ? st[T::NI - 1][3] : st[0][3]));
           }
         }
         st4(la + pix * WG_AS + qh * 4, v);
@@ -173,36 +202,38 @@ __global__ __launch_bounds__(256) void wgrad_kernel(
     }
   };
 
+  // per-lane operand bases; the k-step's own offset is a compile-time immediate
+  const float* aP = lg + (kq + 4 * wk) * GS + wco * 32 + l16;
+  const float* bP = la + (kq + 4 * wk) * WG_AS + wci * 16 + l16;
+
   if (t_beg < t_end) issue(t_beg);
   for (int t = t_beg; t < t_end; ++t) {
     __syncthreads();
     store();
     __syncthreads();
     if (t + 1 < t_end) issue(t + 1);
-    if (blockIdx.z == 0 && tid < CO_T) {
-      float ts = 0.f;
-      for (int px = 0; px < WG_PT; ++px) ts += lg[px * GS + tid];
-      bsum += (double)ts;
-    }
-#pragma unroll 2
-    for (int s = wk; s < WG_PT / 4; s += KSPLIT) {
-      const int px = 4 * s + kq;
-      const int img = px >> g.ltpx, rem = px & (tpx - 1);
-      const int r = rem >> g.lTW, c = rem & (g.TW - 1);
-      const int hb = ((img * HP + r) * WP + c) * WG_AS + wci * 16 + l16;
-      const float a0 = lg[px * GS + wco * 32 + l16];
-      const float a1 = lg[px * GS + wco * 32 + 16 + l16];
+    // one iteration per tile row: its k-steps are unrolled with immediate offsets
+#pragma unroll ROW_UNROLL
+    for (int row = 0; row < T::NI * T::TH; ++row) {
+      const int img = row / T::TH, r = row % T::TH;
+      const float* ap = aP + row * TW * GS;
+      const float* bp = bP + (img * T::HP + r) * T::WP * WG_AS;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int kh = tap / 3, kw = tap % 3;
-        const float bv = la[hb + (kh * WP + kw) * WG_AS];
-        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc[0][tap], 0, 0, 0);
-        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc[1][tap], 0, 0, 0);
+      for (int jj = 0; jj < SPR; ++jj) {
+        const int c = 4 * KSPLIT * jj;
+        const float a0 = ap[c * GS];
+        const float a1 = ap[c * GS + 16];
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const float bv = bp[(c + (tap / 3) * T::WP + tap % 3) * WG_AS];
+          acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc[0][tap], 0, 0, 0);
+          acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc[1][tap], 0, 0, 0);
+        }
       }
     }
   }
+  __syncthreads();
   if (KSPLIT == 2) {   // fold the second K half into the first through LDS
-    __syncthreads();
     float* xs = smem + (size_t)(wave - 2 * NWCO) * 72 * 64;
     if (wk == 1) {
 #pragma unroll
@@ -222,6 +253,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[f][tap][r] += xs[((f * 9 + tap) * 4 + r) * 64 + lane];
     }
+    __syncthreads();
   }
   // partial layout [slice][tap][co][ci]
   const int ci = ci0 + wci * 16 + l16;
@@ -236,7 +268,18 @@ __global__ __launch_bounds__(256) void wgrad_kernel(
           wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] = acc[f][tap][r];
         }
   }
-  if (blockIdx.z == 0 && tid < CO_T) bpart[(size_t)slice * Cout + co0 + tid] = (float)bsum;
+  if (do_bias) {   // threads sharing a channel group fold their sums in a fixed order
+    double* xb = reinterpret_cast<double*>(smem);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xb[i * 256 + tid] = bs[i];
+    __syncthreads();
+    if (tid < CO_T) {
+      const int q = tid >> 2, i = tid & 3;
+      double sum = 0.0;
+      for (int m = q; m < 256; m += QG) sum += xb[i * 256 + m];
+      bpart[(size_t)slice * Cout + co0 + tid] = (float)sum;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ cin == 1 (first conv)
@@ -434,11 +477,11 @@ static size_t wg_lds(int variant, const WgGeom& g, int co_t) {
   return (WG_PT * 48 + halo) * sizeof(float);
 }
 
-template <int NWCO, int KSPLIT, int MODE>
-static void launch_wg(dim3 grid, size_t lds, hipStream_t s, const float* src, const float* st,
-                      const float* gy, float* wpart, float* bpart, int B, int H, int W, int cin,
-                      int cout, const WgGeom& g) {
-  auto k = wgrad_kernel<NWCO, KSPLIT, MODE>;
+template <int NWCO, int KSPLIT, int MODE, int TW>
+static void launch_wg_tw(dim3 grid, size_t lds, hipStream_t s, const float* src, const float* st,
+                         const float* gy, float* wpart, float* bpart, int B, int H, int W, int cin,
+                         int cout, const WgGeom& g) {
+  auto k = wgrad_kernel<NWCO, KSPLIT, MODE, TW>;
   static bool once = false;
   if (!once) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -446,6 +489,18 @@ static void launch_wg(dim3 grid, size_t lds, hipStream_t s, const float* src, co
   }
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, (const float2*)st, gy, wpart, bpart, B, H, W,
                      cin, cout, g);
+}
+
+template <int NWCO, int KSPLIT, int MODE>
+static void launch_wg(dim3 grid, size_t lds, hipStream_t s, const float* src, const float* st,
+                      const float* gy, float* wpart, float* bpart, int B, int H, int W, int cin,
+                      int cout, const WgGeom& g) {
+  if (g.TW == 32)
+    launch_wg_tw<NWCO, KSPLIT, MODE, 32>(grid, lds, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+  else if (g.TW == 16)
+    launch_wg_tw<NWCO, KSPLIT, MODE, 16>(grid, lds, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+  else if constexpr (NWCO == 1)   // 8x8 maps always take the 32-wide co tile
+    launch_wg_tw<NWCO, KSPLIT, MODE, 8>(grid, lds, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
 }
 
 }  // namespace ev
@@ -481,11 +536,14 @@ extern "C" int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, i
   }
   EV_REQUIRE(cin % 32 == 0 && (cout == 32 || cout % 64 == 0), "conv3x3_wgrad: cin=%d cout=%d unsupported",
              cin, cout);
+  EV_REQUIRE((g.TW == 32 && g.TH == 4) || (g.TW == 16 && g.TH == 8 && g.NI == 1) ||
+                 (g.TW == 8 && g.TH == 8 && g.NI == 2),
+             "conv3x3_wgrad: unsupported tile geometry H=%d W=%d", H, W);
   EV_REQUIRE(src_mode != ACT_NORM_POOL,
              "conv3x3_wgrad: pass the pooled activation materialised by the forward (RAW)");
-  if (cout == 32) {
+  if (cout == 32 || g.TW == 8) {
     const size_t lds = wg_lds(0, g, 32);
-    const dim3 grid(g.slices, 1, cin / 32);
+    const dim3 grid(g.slices, cout / 32, cin / 32);
     switch (src_mode) {
       case ACT_RAW: launch_wg<1, 2, ACT_RAW>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;
       case ACT_NORM: launch_wg<1, 2, ACT_NORM>(grid, lds, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g); break;

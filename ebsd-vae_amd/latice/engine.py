@@ -115,10 +115,21 @@ class probe:
         global _PROBE
         _PROBE = None
 
+    def per_tag(self):
+        """{tag: [launches, flops, ms]} (per-layer view for tools/layer_profile.py)."""
+        torch.cuda.synchronize()
+        out = {}
+        for fam, flops, e0, e1, tag in self.records:
+            d = out.setdefault(f"{fam} {tag}", [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += flops
+            d[2] += e0.elapsed_time(e1)
+        return out
+
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for fam, flops, e0, e1 in self.records:
+        for fam, flops, e0, e1, _ in self.records:
             d = out.setdefault(fam, {"launches": 0, "flops": 0.0, "ms": 0.0})
             d["launches"] += 1
             d["flops"] += flops
@@ -126,7 +137,7 @@ class probe:
         return out
 
 
-def _launch(family, flops, fn, *args):
+def _launch(family, flops, fn, *args, tag=None):
     if _PROBE is None:
         return fn(*args)
     e0 = torch.cuda.Event(enable_timing=True)
@@ -134,7 +145,7 @@ def _launch(family, flops, fn, *args):
     e0.record()
     r = fn(*args)
     e1.record()
-    _PROBE.append((family, float(flops), e0, e1))
+    _PROBE.append((family, float(flops), e0, e1, tag))
     return r
 
 
@@ -167,7 +178,8 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False):
     act = _empty(B, H, H, layer.cin, like=w) if keep_act else None
     _launch("conv3x3_fwd", conv_flops(B, H, H, layer.cin, layer.cout), N.call,
             "ebsdvae_conv3x3_fwd", N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp), N.ptr(b),
-            N.ptr(y), N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout, N.stream())
+            N.ptr(y), N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout, N.stream(),
+            tag=f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m{layer.src_mode}")
     st = _empty(B, layer.cout, 2, like=w)
     N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
            N.stream())
@@ -251,7 +263,8 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
     s = N.stream()
     _launch("conv3x3_wgrad", conv_flops(B, H, W, cin, cout), N.call,
             "ebsdvae_conv3x3_wgrad", N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(gy),
-            N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout, s)
+            N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout, s,
+            tag=f"wgrad {cin:3d}->{cout:3d} @{H:3d} m{src_mode}")
     nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
     work = torch.empty(nbytes // 8, dtype=torch.float64, device=gy.device)
     N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db),
@@ -264,7 +277,8 @@ def conv_dgrad(gy, layer: ConvLayer, w):
     gin = _empty(B, H, W, layer.cin, like=gy)
     _launch("conv3x3_fwd", conv_flops(B, H, W, layer.cin, layer.cout), N.call,
             "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(wd), None, N.ptr(gin), None,
-            None, B, H, W, layer.cout, layer.cin, N.stream())
+            None, B, H, W, layer.cout, layer.cin, N.stream(),
+            tag=f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}")
     return gin
 
 
