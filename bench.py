@@ -52,6 +52,20 @@ def step_flops_per_pattern(plan) -> float:
     return f + 3 * lin
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(fam: str):
+    """HBM bytes per launch of `fam` from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 fetch correction)."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            t = json.load(f)["traffic"][fam]
+        return t["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(plan, seconds: float, batch: int):
     from latice.seeding import seeded_state_dict, synthetic_patterns
     from oracle.torch_port import CPUStep   # oracle: the baseline leg only
@@ -160,7 +174,7 @@ def main():
         ach = flops_per_launch / avg_s / 1e12
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": pmc_traffic(dom),
                 "launches_per_step": d["launches"] // args.steps,
                 "avg_launch_us": round(avg_s * 1e6, 2),
                 "gflop_per_launch": round(flops_per_launch / 1e9, 3)}
