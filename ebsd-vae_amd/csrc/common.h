@@ -28,9 +28,14 @@ enum ActMode : int {
   ACT_NORM_UP = 4,    // ACT_NORM of src at half resolution, nearest x2
 };
 
-EV_DEVINL float lrelu(float v) { return v > 0.f ? v : kSlope * v; }
+// max(v, slope*v) == (v > 0 ? v : slope*v) bit for bit for 0 < slope < 1 (2 VALU ops)
+EV_DEVINL float lrelu(float v) { return fmaxf(v, kSlope * v); }
 
 EV_DEVINL float normact(float v, float2 st) { return lrelu((v - st.x) * st.y); }
+
+// {mean, rstd} -> {rstd, -mean*rstd}: normact as one FMA + lrelu (staging hot loops)
+EV_DEVINL float2 norm_fs(float2 st) { return make_float2(st.y, -st.x * st.y); }
+EV_DEVINL float normact_fs(float v, float2 fs) { return lrelu(fmaf(v, fs.x, fs.y)); }
 
 EV_DEVINL float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 EV_DEVINL void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }

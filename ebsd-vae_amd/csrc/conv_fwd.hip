@@ -160,7 +160,16 @@ __global__ __launch_bounds__(NWV * 64) void conv3x3_big_kernel(
   const float* sb = src + (size_t)b0 * Hs * Ws * Cin;
   const int q = tid & 1;  // this thread's 4-channel half of every 8-channel chunk
 
-  // halo item k of this thread: pixel (tid + NTHR*k) >> 1, channels q*4..q*4+3
+  // halo item k of this thread: pixel (tid + NTHR*k) >> 1, channels q*4..q*4+3.  Its
+  // source coordinates are chunk-invariant: packed once as (gh << 16) | gw, -1 = zero pad.
+  int hw[KX];
+#pragma unroll
+  for (int k = 0; k < KX; ++k) {
+    const int pix = (tid + NTHR * k) >> 1;
+    const int hh = pix / WP, ww = pix - hh * WP;
+    const int gh = h0 + hh - 1, gw = ww - 1;
+    hw[k] = (pix < pixP && gh >= 0 && gh < H && gw >= 0 && gw < W) ? ((gh << 16) | gw) : -1;
+  }
   float4 raw[KX][NR];
   float2 st[4];
   int cur_ch = 0;   // chunk whose halo is held in raw[]
@@ -169,11 +178,8 @@ __global__ __launch_bounds__(NWV * 64) void conv3x3_big_kernel(
     const int c = ch * CK + q * 4;
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
-      const int pix = (tid + NTHR * k) >> 1;
-      const int hh = pix / WP, ww = pix - hh * WP;
-      const int gh = h0 + hh - 1, gw = ww - 1;
-      const bool ok = (pix < pixP) && gh >= 0 && gh < H && gw >= 0 && gw < W;
-      if (ok) {
+      if (hw[k] >= 0) {
+        const int gh = hw[k] >> 16, gw = hw[k] & 0xffff;
         if (POOL) {
           const float* p = sb + ((size_t)(2 * gh) * Ws + 2 * gw) * Cin + c;
           const size_t rs = (size_t)Ws * Cin;
@@ -194,28 +200,31 @@ __global__ __launch_bounds__(NWV * 64) void conv3x3_big_kernel(
     }
   };
   auto store_halo = [&](float* lx) {
+    float2 fs[4];
+    if (NORM) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fs[i] = norm_fs(st[i]);
+    }
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
       const int pix = (tid + NTHR * k) >> 1;
       if (pix < pixP) {
-        const int hh = pix / WP, ww = pix - hh * WP;
-        const int gh = h0 + hh - 1, gw = ww - 1;
-        const bool ok = gh >= 0 && gh < H && gw >= 0 && gw < W;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) {
+        if (hw[k] >= 0) {
           v = raw[k][0];
           if (POOL)
             v = max4(max4(raw[k][0], raw[k][NR > 1 ? 1 : 0]),
                      max4(raw[k][NR > 2 ? 2 : 0], raw[k][NR > 3 ? 3 : 0]));
           if (NORM)
-            v = make_float4(normact(v.x, st[0]), normact(v.y, st[1]), normact(v.z, st[2]),
-                            normact(v.w, st[3]));
+            v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]),
+                            normact_fs(v.z, fs[2]), normact_fs(v.w, fs[3]));
+          // interior pixels: optionally materialise the (pooled) activation for the wgrad
+          const int gh = hw[k] >> 16, gw = hw[k] & 0xffff;
+          if (act_out && gh >= h0 && gh < h0 + TH)
+            st4(act_out + (((size_t)b0 * H + gh) * W + gw) * Cin + cur_ch * CK + q * 4, v);
         }
         float* d = lx + pix * CKP + q * 4;
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        // interior pixels: optionally materialise the (pooled) activation for the wgrad
-        if (act_out && ok && hh >= 1 && hh <= TH)
-          st4(act_out + (((size_t)b0 * H + gh) * W + gw) * Cin + cur_ch * CK + q * 4, v);
       }
     }
   };
