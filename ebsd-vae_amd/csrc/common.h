@@ -33,6 +33,11 @@ EV_DEVINL float lrelu(float v) { return fmaxf(v, kSlope * v); }
 
 EV_DEVINL float normact(float v, float2 st) { return lrelu((v - st.x) * st.y); }
 
+// how a block's output reaches its consumer (InstanceNorm backward routing)
+enum PMode : int { P_ID = 0, P_POOL = 1, P_UP = 2 };
+// d lrelu / d xhat
+EV_DEVINL float slope(float xh) { return xh > 0.f ? 1.f : kSlope; }
+
 // {mean, rstd} -> {rstd, -mean*rstd}: normact as one FMA + lrelu (staging hot loops)
 EV_DEVINL float2 norm_fs(float2 st) { return make_float2(st.y, -st.x * st.y); }
 EV_DEVINL float normact_fs(float v, float2 fs) { return lrelu(fmaf(v, fs.x, fs.y)); }

@@ -42,15 +42,51 @@ EV_DEVINL void glds16(const float* g, float* lds_wave_base) {
 }
 
 // ------------------------------------------------------------------ shared epilogue
-template <int MF, int NF>
+constexpr int FP_NONE = -1;   // no fused InstanceNorm-backward reduce
+
+// Fused InstanceNorm-backward reduce of the PREVIOUS block (input-gradient convs only):
+// this conv's output is g = d loss / d a_prev (a_prev = [pool|up](lrelu(IN(y_prev))) at
+// this conv's resolution).  Per element it adds g_a = g * lrelu'(xhat) and g_a * xhat of
+// the y_prev pixel that g routes to (identity, the 2x2 argmax, or the upsample parent)
+// -- the sums ebsdvae_in_bwd_reduce would compute, without re-reading g.
+// y_prev offset (in pixels of y_prev) of the k-th value read for conv pixel pl
+template <int FP>
+EV_DEVINL int inbwd_pix(int pl, int W, int lW, int k) {
+  const int h = pl >> lW, w = pl & (W - 1);
+  if (FP == P_ID) return pl;
+  if (FP == P_UP) return (h >> 1) * (W >> 1) + (w >> 1);
+  return (2 * h + (k >> 1)) * (2 * W) + 2 * w + (k & 1);   // P_POOL window (k = dy*2+dx)
+}
+
+template <int FP>
+EV_DEVINL void inbwd_acc(float g, const float* v, float2 sp, float& s1, float& s2) {
+  float x = (v[0] - sp.x) * sp.y;
+  if (FP == P_POOL) {   // first maximum of lrelu(xhat) in window order (0,0),(0,1),(1,0),(1,1)
+    float best = lrelu(x);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float xk = (v[k] - sp.x) * sp.y;
+      const float f = lrelu(xk);
+      if (f > best) { best = f; x = xk; }
+    }
+  }
+  const float ga = g * slope(x);
+  s1 += ga;
+  s2 = fmaf(ga, x, s2);
+}
+
+template <int MF, int NF, int FP>
 EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bias,
                              float* __restrict__ y, float2* __restrict__ spart, int B, int H,
                              int W, int Cout, int b0, int h0, int tpx, int wpx0, int co_base,
-                             int hk, int l32) {
+                             int hk, int l32, const float* __restrict__ yprev,
+                             const float2* __restrict__ stprev, double2* __restrict__ ipart) {
   constexpr int MW = MF * 32;
   const int wimg = wpx0 / tpx;  // the wave's pixels lie in ONE image
   const int gb = b0 + wimg;
   const bool bvalid = gb < B;
+  const int T = (H * W) / MW;
+  const int slot = (h0 * W + (wpx0 - wimg * tpx)) / MW;
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf) {
     const int co = co_base + nf * 32 + l32;
@@ -67,6 +103,37 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         s += v;
         if (bvalid) y[(((size_t)gb * H + h0) * W + rem) * Cout + co] = v;
       }
+    if (FP != FP_NONE && bvalid) {
+      // loads in batches of 32 issued before any use (latency overlapped within a batch)
+      constexpr int NL = FP == P_POOL ? 4 : 1;
+      constexpr int G = (32 / NL) < MF * 16 ? (32 / NL) : MF * 16;
+      static_assert((MF * 16) % G == 0, "batch size");
+      const int lW = 31 - __builtin_clz(W);
+      const size_t plane = FP == P_POOL ? (size_t)4 * H * W : (FP == P_UP ? (size_t)(H * W) / 4 : (size_t)H * W);
+      const float* yp = yprev + (size_t)gb * plane * Cout + co;
+      const float2 sp = stprev[(size_t)gb * Cout + co];
+      const int pbase = h0 * W - wimg * tpx + wpx0 + 4 * hk;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e0 = 0; e0 < MF * 16; e0 += G) {
+        float v[G][NL];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const int e = e0 + j, mf = e >> 4, r = e & 15;
+          const int pl = pbase + mf * 32 + (r & 3) + 8 * (r >> 2);
+#pragma unroll
+          for (int k = 0; k < NL; ++k) v[j][k] = yp[(size_t)inbwd_pix<FP>(pl, W, lW, k) * Cout];
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const int e = e0 + j;
+          inbwd_acc<FP>(acc[e >> 4][nf][e & 15], v[j], sp, s1, s2);
+        }
+      }
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (hk == 0) ipart[((size_t)gb * T + slot) * Cout + co] = make_double2((double)s1, (double)s2);
+    }
     if (spart) {
       s += __shfl_xor(s, 32, 64);
       const float mean = s * (1.0f / MW);
@@ -79,11 +146,7 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
           q = fmaf(d, d, q);
         }
       q += __shfl_xor(q, 32, 64);
-      if (hk == 0 && bvalid) {
-        const int T = (H * W) / MW;
-        const int slot = (h0 * W + (wpx0 - wimg * tpx)) / MW;
-        spart[((size_t)gb * T + slot) * Cout + co] = make_float2(mean, q);
-      }
+      if (hk == 0 && bvalid) spart[((size_t)gb * T + slot) * Cout + co] = make_float2(mean, q);
     }
   }
 }
@@ -117,11 +180,12 @@ EV_DEVINL void mma_chunk(f32x16 (&acc)[MF][NF], const float* __restrict__ lx,
 // ------------------------------------------------------------------ main pipelined kernel
 // 8 waves as WM (pixels) x WN (channels); KX = halo float4 items per thread (compile-time
 // upper bound); MODE = act source mode.
-template <int NWV, int WM, int MF, int NF, int KX, int MODE>
-__global__ __launch_bounds__(NWV * 64) void conv3x3_big_kernel(
+template <int NWV, int WM, int MF, int NF, int KX, int MODE, int FP>
+__global__ __launch_bounds__(NWV * 64, 2) void conv3x3_big_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, const float* __restrict__ wp,
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
-    float* __restrict__ act_out, int B, int H, int W, int Cin, int TH) {
+    float* __restrict__ act_out, int B, int H, int W, int Cin, int TH,
+    const float* __restrict__ yprev, const float2* __restrict__ stprev, double2* __restrict__ ipart) {
   constexpr int WN = NWV / WM;
   constexpr int NT = WN * NF * 32;   // == Cout
   constexpr int MW = MF * 32;
@@ -258,18 +322,20 @@ __global__ __launch_bounds__(NWV * 64) void conv3x3_big_kernel(
     if (more) store_halo(lx0 + nxt * xslab);
     __syncthreads();
   }
-  conv_epilogue<MF, NF>(acc, bias, y, spart, B, H, W, NT, b0, h0, tpx, wm * MW, wn * NF * 32, hk, l32);
+  conv_epilogue<MF, NF, FP>(acc, bias, y, spart, B, H, W, NT, b0, h0, tpx, wm * MW, wn * NF * 32, hk,
+                            l32, yprev, stprev, ipart);
 }
 
 // ------------------------------------------------------------------ small-image kernel
 // 256 threads; TH-row bands (whole 8x8 images) per block; Cout split into NT-wide column
 // blocks over blockIdx.y.  CIN1: K = the 9 taps (first conv), NI images per block.
-template <int WM, int MF, int NF, bool CIN1>
+template <int WM, int MF, int NF, bool CIN1, int FP>
 __global__ __launch_bounds__(256) void conv3x3_small_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, int smode,
     const float* __restrict__ wp, const float* __restrict__ bias, float* __restrict__ y,
     float2* __restrict__ spart, float* __restrict__ act_out, int B, int H, int W, int Cin, int Cout,
-    int TH, int NI) {
+    int TH, int NI, const float* __restrict__ yprev, const float2* __restrict__ stprev,
+    double2* __restrict__ ipart) {
   constexpr int WN = 4 / WM;
   constexpr int NT = WN * NF * 32;
   constexpr int MW = MF * 32;
@@ -365,8 +431,8 @@ __global__ __launch_bounds__(256) void conv3x3_small_kernel(
       mma_chunk<MF, NF>(acc, lx, lw, abase, WP, NT, ncol, hk);
     }
   }
-  conv_epilogue<MF, NF>(acc, bias, y, spart, B, H, W, Cout, b0, h0, tpx, wm * MW, n0 + wn * NF * 32,
-                        hk, l32);
+  conv_epilogue<MF, NF, FP>(acc, bias, y, spart, B, H, W, Cout, b0, h0, tpx, wm * MW,
+                            n0 + wn * NF * 32, hk, l32, yprev, stprev, ipart);
 }
 
 // Weight packing into [chunk][tap][ci8][Cout'] (CK = 8; CK = 1 when Cin' == 1).
@@ -452,40 +518,59 @@ static void allow_big_lds(K k) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-template <int NWV, int WM, int MF, int NF, int KX, int MODE>
+// fused InstanceNorm-backward reduce arguments of input-gradient launches (FP != FP_NONE)
+struct InBwdFuse {
+  const float* yprev = nullptr;
+  const float2* stprev = nullptr;
+  double2* part = nullptr;
+};
+
+template <int NWV, int WM, int MF, int NF, int KX, int MODE, int FP>
 static void launch_big1(const Cfg& c, const float* src, const float* st, const float* wp,
                         const float* bias, float* y, float* part, float* aout, int B, int H, int W,
-                        int cin, hipStream_t s) {
-  auto k = conv3x3_big_kernel<NWV, WM, MF, NF, KX, MODE>;
+                        int cin, hipStream_t s, const InBwdFuse& f) {
+  auto k = conv3x3_big_kernel<NWV, WM, MF, NF, KX, MODE, FP>;
   static bool once = false;
   if (!once) { allow_big_lds(k); once = true; }
   hipLaunchKernelGGL(k, dim3(B * (H / c.TH)), dim3(NWV * 64), c.lds, s, src, (const float2*)st, wp, bias,
-                     y, (float2*)part, aout, B, H, W, cin, c.TH);
+                     y, (float2*)part, aout, B, H, W, cin, c.TH, f.yprev, f.stprev, f.part);
 }
 
 template <int NWV, int WM, int MF, int NF, int KX>
 static void launch_big(const Cfg& c, const float* src, const float* st, int mode, const float* wp,
                        const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                        int cin, hipStream_t s) {
+  const InBwdFuse f;
   switch (mode) {
-    case ACT_RAW: launch_big1<NWV, WM, MF, NF, KX, ACT_RAW>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s); break;
-    case ACT_NORM: launch_big1<NWV, WM, MF, NF, KX, ACT_NORM>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s); break;
-    case ACT_NORM_POOL: launch_big1<NWV, WM, MF, NF, KX, ACT_NORM_POOL>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s); break;
-    case ACT_UP: launch_big1<NWV, WM, MF, NF, KX, ACT_UP>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s); break;
-    default: launch_big1<NWV, WM, MF, NF, KX, ACT_NORM_UP>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s); break;
+    case ACT_RAW: launch_big1<NWV, WM, MF, NF, KX, ACT_RAW, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_NORM: launch_big1<NWV, WM, MF, NF, KX, ACT_NORM, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_NORM_POOL: launch_big1<NWV, WM, MF, NF, KX, ACT_NORM_POOL, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_UP: launch_big1<NWV, WM, MF, NF, KX, ACT_UP, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    default: launch_big1<NWV, WM, MF, NF, KX, ACT_NORM_UP, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
   }
 }
 
-template <int WM, int MF, int NF, bool CIN1>
+template <int NWV, int WM, int MF, int NF, int KX>
+static void launch_big_fused(const Cfg& c, const float* src, const float* wp, float* y, int B, int H,
+                             int W, int cin, hipStream_t s, int pmode, const InBwdFuse& f) {
+  switch (pmode) {
+    case P_ID: launch_big1<NWV, WM, MF, NF, KX, ACT_RAW, P_ID>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+    case P_POOL: launch_big1<NWV, WM, MF, NF, KX, ACT_RAW, P_POOL>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+    default: launch_big1<NWV, WM, MF, NF, KX, ACT_RAW, P_UP>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+  }
+}
+
+template <int WM, int MF, int NF, bool CIN1, int FP>
 static void launch_small(const Cfg& c, const float* src, const float* st, int mode, const float* wp,
                          const float* bias, float* y, float* part, float* aout, int B, int H, int W,
-                         int cin, int cout, hipStream_t s) {
-  auto k = conv3x3_small_kernel<WM, MF, NF, CIN1>;
+                         int cin, int cout, hipStream_t s, const InBwdFuse& f = InBwdFuse()) {
+  auto k = conv3x3_small_kernel<WM, MF, NF, CIN1, FP>;
   static bool once = false;
   if (!once) { allow_big_lds(k); once = true; }
   const int bx = (c.NI > 1) ? (B + c.NI - 1) / c.NI : B * (H / c.TH);
   hipLaunchKernelGGL(k, dim3(bx, cout / c.NT), dim3(256), c.lds, s, src, (const float2*)st, mode, wp,
-                     bias, y, (float2*)part, aout, B, H, W, cin, cout, c.TH, c.NI);
+                     bias, y, (float2*)part, aout, B, H, W, cin, cout, c.TH, c.NI, f.yprev, f.stprev,
+                     f.part);
 }
 
 }  // namespace ev
@@ -525,9 +610,9 @@ extern "C" int ebsdvae_conv3x3_fwd(const float* src, const float* src_stats, int
              H, W, cin, cout);
   hipStream_t s = (hipStream_t)stream;
   if (c.kind == 2) {
-    launch_small<4, 4, 1, true>(c, src, src_stats, src_mode, wpack, bias, y, stat_part, act_out, B, H, W, cin, cout, s);
+    launch_small<4, 4, 1, true, FP_NONE>(c, src, src_stats, src_mode, wpack, bias, y, stat_part, act_out, B, H, W, cin, cout, s);
   } else if (c.kind == 1) {
-    launch_small<2, 1, 1, false>(c, src, src_stats, src_mode, wpack, bias, y, stat_part, act_out, B, H, W, cin, cout, s);
+    launch_small<2, 1, 1, false, FP_NONE>(c, src, src_stats, src_mode, wpack, bias, y, stat_part, act_out, B, H, W, cin, cout, s);
   } else if (cout == 128) {
     launch_big<8, 4, 2, 2, 2>(c, src, src_stats, src_mode, wpack, bias, y, stat_part, act_out, B, H, W, cin, s);
   } else if (cout == 64) {
@@ -536,4 +621,37 @@ extern "C" int ebsdvae_conv3x3_fwd(const float* src, const float* src_stats, int
     launch_big<4, 4, 4, 1, 9>(c, src, src_stats, src_mode, wpack, bias, y, stat_part, act_out, B, H, W, cin, s);
   }
   return evh::check_launch("conv3x3_fwd");
+}
+
+extern "C" int ebsdvae_conv3x3_dgrad_inbwd(const float* g, const float* wpack, float* gin,
+                                           const float* y_prev, const float* st_prev, int pmode,
+                                           double* part, int B, int H, int W, int cin, int cout,
+                                           ebsdvae_stream_t stream) {
+  Cfg c;
+  EV_REQUIRE(g && wpack && gin && y_prev && st_prev && part && B > 0,
+             "conv3x3_dgrad_inbwd: null pointer or empty batch");
+  EV_REQUIRE(pmode == P_ID || pmode == P_POOL || pmode == P_UP, "conv3x3_dgrad_inbwd: bad pmode %d", pmode);
+  EV_REQUIRE(cin % CK == 0 && (W & (W - 1)) == 0 && (pmode != P_UP || (H % 2 == 0 && W % 2 == 0)),
+             "conv3x3_dgrad_inbwd: cin=%d W=%d unsupported", cin, W);
+  EV_REQUIRE(plan_conv(H, W, cin, cout, &c) && c.kind != 2,
+             "conv3x3_dgrad_inbwd: unsupported shape H=%d W=%d cin=%d cout=%d", H, W, cin, cout);
+  hipStream_t s = (hipStream_t)stream;
+  InBwdFuse f;
+  f.yprev = y_prev;
+  f.stprev = (const float2*)st_prev;
+  f.part = (double2*)part;
+  if (c.kind == 1) {
+    switch (pmode) {
+      case P_ID: launch_small<2, 1, 1, false, P_ID>(c, g, nullptr, ACT_RAW, wpack, nullptr, gin, nullptr, nullptr, B, H, W, cin, cout, s, f); break;
+      case P_POOL: launch_small<2, 1, 1, false, P_POOL>(c, g, nullptr, ACT_RAW, wpack, nullptr, gin, nullptr, nullptr, B, H, W, cin, cout, s, f); break;
+      default: launch_small<2, 1, 1, false, P_UP>(c, g, nullptr, ACT_RAW, wpack, nullptr, gin, nullptr, nullptr, B, H, W, cin, cout, s, f); break;
+    }
+  } else if (cout == 128) {
+    launch_big_fused<8, 4, 2, 2, 2>(c, g, wpack, gin, B, H, W, cin, s, pmode, f);
+  } else if (cout == 64) {
+    launch_big_fused<4, 4, 2, 2, 5>(c, g, wpack, gin, B, H, W, cin, s, pmode, f);
+  } else {
+    launch_big_fused<4, 4, 4, 1, 9>(c, g, wpack, gin, B, H, W, cin, s, pmode, f);
+  }
+  return evh::check_launch("conv3x3_dgrad_inbwd");
 }

@@ -16,10 +16,6 @@
 
 namespace ev {
 
-enum PMode : int { P_ID = 0, P_POOL = 1, P_UP = 2 };
-
-EV_DEVINL float slope(float xh) { return xh > 0.f ? 1.f : kSlope; }
-
 // One workgroup per pattern b: thread (c = tid % C, j = tid / C) folds tiles j, j+J, ... of
 // channel c (coalesced over c), then lane j == 0 folds the J partial results in order.
 // All tiles hold n elements, so the Chan merge reduces to: mean = avg(mean_t),

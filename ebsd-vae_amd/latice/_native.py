@@ -28,6 +28,7 @@ SIGNATURES = {
     "ebsdvae_pack_conv_weight": [P, P, I, I, I, I, P],
     "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_stat_tiles": [I, I, I],
+    "ebsdvae_conv3x3_dgrad_inbwd": [P, P, P, P, P, I, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_fwd": [P, P, I, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],
     "ebsdvae_conv3x3_wgrad_slices": [I, I, I, I, I],

@@ -188,14 +188,18 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False):
     return y, st
 
 
-def in_backward(gnext, pmode, y, st):
-    """gy = d loss / d y through [pool|up] . lrelu . InstanceNorm of one block."""
+def in_backward(gnext, pmode, y, st, part=None):
+    """gy = d loss / d y through [pool|up] . lrelu . InstanceNorm of one block.
+    part: the reduce-pass sums already produced by the fused input-gradient conv that
+    computed gnext (conv_dgrad(..., prev=...)); None runs the reduce pass here."""
     B, H, W, C = y.shape
-    T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
-    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
     s = N.stream()
-    N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), part.data_ptr(),
-           B, H, W, C, s)
+    if part is None:
+        T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
+        part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
+        N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), part.data_ptr(),
+               B, H, W, C, s)
+    T = part.shape[1]
     bst = _empty(B, C, 2, like=y)
     N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, T, H * W, s)
     gy = torch.empty_like(y)
@@ -236,16 +240,19 @@ def in_backward_final(g1, w14, y, st, dw14, db14):
     return gy
 
 
-def in_backward_first(gnext, y, st, x, dw0, db0):
+def in_backward_first(gnext, y, st, x, dw0, db0, part=None):
     """Backward of the first conv block (latice/model.py:110): writes dW/db of the 1->32
-    conv directly from the InstanceNorm-backward apply pass (gy is never materialised)."""
+    conv directly from the InstanceNorm-backward apply pass (gy is never materialised).
+    part: reduce-pass sums from the fused input-gradient conv (None: reduce here)."""
     B, H, W, C = y.shape
+    if part is None:
+        T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
+        part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
+        N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), P_ID, N.ptr(y), N.ptr(st), part.data_ptr(),
+               B, H, W, C, N.stream())
+    bst = _in_bwd_stats(B, C, part.shape[1], H * W, part, y)
     T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
     S_ = B * T
-    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
-    N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), P_ID, N.ptr(y), N.ptr(st), part.data_ptr(),
-           B, H, W, C, N.stream())
-    bst = _in_bwd_stats(B, C, T, H * W, part, y)
     wpart = _empty(S_, 9, C, 1, like=y)
     bpart = _empty(S_, C, like=y)
     N.call("ebsdvae_in_bwd_first_apply_wgrad", N.ptr(gnext), N.ptr(y), N.ptr(st), N.ptr(bst),
@@ -271,15 +278,27 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
            cin, cout, kind, work.data_ptr(), s)
 
 
-def conv_dgrad(gy, layer: ConvLayer, w):
+def conv_dgrad(gy, layer: ConvLayer, w, prev=None):
+    """Input gradient of `layer`.  prev = (y_prev, st_prev, pmode_prev) of the block feeding
+    it: the previous block's InstanceNorm-backward reduce is then fused into the epilogue and
+    (gin, part) is returned for in_backward(..., part=part)."""
     B, H, W, _ = gy.shape
     wd = pack_weight(w, layer, dgrad=True)
     gin = _empty(B, H, W, layer.cin, like=gy)
-    _launch("conv3x3_fwd", conv_flops(B, H, W, layer.cin, layer.cout), N.call,
-            "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(wd), None, N.ptr(gin), None,
-            None, B, H, W, layer.cout, layer.cin, N.stream(),
-            tag=f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}")
-    return gin
+    tag = f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}"
+    flops = conv_flops(B, H, W, layer.cin, layer.cout)
+    if prev is None:
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW,
+                N.ptr(wd), None, N.ptr(gin), None, None, B, H, W, layer.cout, layer.cin,
+                N.stream(), tag=tag)
+        return gin
+    y_prev, st_prev, pmode = prev
+    T = N.call("ebsdvae_conv3x3_stat_tiles", H, W, layer.cin)
+    part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
+    _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd", N.ptr(gy), N.ptr(wd),
+            N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev), pmode, part.data_ptr(), B, H, W,
+            layer.cout, layer.cin, N.stream(), tag=tag + " +inbwd")
+    return gin, part
 
 
 def _grad_buf(grads, name, like):
@@ -313,7 +332,7 @@ def encoder_forward(plan: Plan, x, params):
 def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=False):
     """g_enc: grad of the encoder output (B,s,s,C) NHWC.  Returns (grads dict, gx or None)."""
     out = {}
-    g_next = g_enc
+    g_next, part = g_enc, None
     gx = None
     for i in reversed(range(len(plan.enc))):
         L = plan.enc[i]
@@ -323,10 +342,10 @@ def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=Fa
             wn, bn = L.name + ".weight", L.name + ".bias"
             dw = _grad_buf(grads, wn, params[wn])
             db = _grad_buf(grads, bn, params[bn])
-            in_backward_first(g_next, y, st, x, dw, db)
+            in_backward_first(g_next, y, st, x, dw, db, part=part)
             out[wn], out[bn] = dw, db
             break
-        gy = in_backward(g_next, L.pmode, y, st)
+        gy = in_backward(g_next, L.pmode, y, st, part=part)
         mode = L.src_mode
         if i == 0:
             src, sst = x, None
@@ -340,7 +359,8 @@ def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=Fa
         conv_wgrad(src, sst, mode, gy, L.cin, L.cout, L.kind, dw, db)
         out[wn], out[bn] = dw, db
         if i > 0:
-            g_next = conv_dgrad(gy, L, params[wn])
+            P = plan.enc[i - 1]
+            g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode))
         elif need_gx:
             B, H, W, _ = gy.shape
             gx = _empty(B, 1, H, W, like=gy)
@@ -416,18 +436,22 @@ def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None):
     # recomputed from g1 on the fly, its weight gradient accumulated in the reduce pass
     gy_last = in_backward_final(g1, params[wn], y13, st13, dw, db)
     out[wn], out[bn] = dw, db
-    g_next = None
+    g_next, part = None, None
     for i in reversed(range(len(plan.dec))):
         L = plan.dec[i]
         y, st = saved[L.name]
-        gy = gy_last if i == len(plan.dec) - 1 else in_backward(g_next, L.pmode, y, st)
+        gy = gy_last if i == len(plan.dec) - 1 else in_backward(g_next, L.pmode, y, st, part=part)
         wn, bn = L.name + ".weight", L.name + ".bias"
         src, sst = (saved["__dec_in__"], None) if i == 0 else saved[plan.dec[i - 1].name]
         dw = _grad_buf(grads, wn, params[wn])
         db = _grad_buf(grads, bn, params[bn])
         conv_wgrad(src, sst, L.src_mode, gy, L.cin, L.cout, L.kind, dw, db)
         out[wn], out[bn] = dw, db
-        g_next = conv_dgrad(gy, L, params[wn])
+        if i > 0:
+            P = plan.dec[i - 1]
+            g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode))
+        else:
+            g_next = conv_dgrad(gy, L, params[wn])
     s, C = plan.enc_side, plan.enc_channels
     g_dec = _empty(B, s, s, C, like=g_xhat)
     N.call("ebsdvae_upsample2_bwd", N.ptr(g_next), N.ptr(g_dec), B, s, s, C, N.stream())

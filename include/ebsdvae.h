@@ -62,6 +62,20 @@ int ebsdvae_conv3x3_fwd(const float* src, const float* src_stats, int src_mode,
                         ebsdvae_stream_t stream);
 int ebsdvae_conv3x3_stat_tiles(int H, int W, int cout);
 
+/* Input gradient of a conv (ebsdvae_conv3x3_fwd with a for_dgrad pack and RAW source:
+ * gin = d loss / d a_prev at (B,H,W,cout) NHWC) fused with the reduce pass of the
+ * PREVIOUS block's InstanceNorm backward (ebsdvae_in_bwd_reduce(gin, pmode, y_prev,
+ * st_prev, ...)).  a_prev = pmode(lrelu(IN(y_prev))); y_prev is (B,2H,2W,cout) for P_POOL,
+ * (B,H/2,W/2,cout) for P_UP, (B,H,W,cout) for P_ID.  part receives double2
+ * {sum g_a, sum g_a*xhat} per (b, tile, c) with ebsdvae_conv3x3_stat_tiles(H,W,cout) tiles
+ * per image; ebsdvae_in_bwd_finalize(part, ..., tiles, HW of y_prev) turns them into the
+ * apply-pass statistics.  Replaces autograd's conv input gradient plus the first half of
+ * the InstanceNorm backward (latice/model.py:95-97,102-106).  W must be a power of two. */
+int ebsdvae_conv3x3_dgrad_inbwd(const float* g, const float* wpack, float* gin,
+                                const float* y_prev, const float* st_prev, int pmode,
+                                double* part, int B, int H, int W, int cin, int cout,
+                                ebsdvae_stream_t stream);
+
 /* 3x3 conv with a single output channel (the final nn.Conv2d(32,1), latice/model.py:148):
  * out[b,h,w] = bias + sum act(src)*w[ci][tap'] with tap' = flip ? 8-tap : tap.
  * w is (1,cin,3,3) contiguous (== (cin,1,3,3)).  With flip=1, RAW source and

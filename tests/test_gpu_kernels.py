@@ -158,6 +158,42 @@ def test_instance_norm_backward(cuda, pmode, H, C):
     assert O.rel_err(host(gy), ref) < 1e-4
 
 
+FUSED_CASES = [  # (layer cin, layer cout, H, pmode of the block feeding the layer)
+    (32, 32, 128, E.P_ID), (32, 64, 64, E.P_POOL), (64, 128, 32, E.P_POOL), (128, 128, 16, E.P_UP),
+    (128, 128, 8, E.P_POOL), (128, 128, 8, E.P_ID), (64, 32, 64, E.P_UP), (128, 64, 32, E.P_ID),
+]
+
+
+@pytest.mark.parametrize("cin,cout,H,pmode", FUSED_CASES)
+def test_dgrad_fused_instance_norm_backward(cuda, cin, cout, H, pmode):
+    """Input-gradient conv with the previous block's InstanceNorm-backward reduce fused in
+    its epilogue == conv dgrad, then the unfused IN backward (oracle)."""
+    rng = np.random.default_rng(5 + cin + cout + H + pmode)
+    B = 2
+    Hy = {E.P_ID: H, E.P_POOL: 2 * H, E.P_UP: H // 2}[pmode]
+    y = rng.standard_normal((B, Hy, Hy, cin)) * 2 + 0.5
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    gy = rng.standard_normal((B, H, H, cout))
+    wsrc = rng.standard_normal((cout, cin, 3, 3)) * 0.1
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, E.ACT_RAW, 0)
+    y_d, st_d = dev(y), dev(st)
+    gin, part = E.conv_dgrad(dev(gy), layer, dev(wsrc), prev=(y_d, st_d, pmode))
+    g_prev = E.in_backward(gin, pmode, y_d, st_d, part=part)
+    gn = O.conv3x3_dgrad(gy, wsrc)
+    assert O.rel_err(host(gin), gn) < TOL
+    a = O.lrelu(xh)
+    if pmode == E.P_POOL:
+        _, arg = O.maxpool2(a)
+        ga = O.maxpool2_bwd(gn, arg)
+    elif pmode == E.P_UP:
+        ga = O.upsample2_bwd(gn)
+    else:
+        ga = gn
+    ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
+    assert O.rel_err(host(g_prev), ref) < 1e-4
+
+
 def test_act_apply_and_upsample_bwd(cuda):
     rng = np.random.default_rng(5)
     s, mean, rstd, st = make_src(rng, 3, 4, 128, E.ACT_NORM_POOL)
