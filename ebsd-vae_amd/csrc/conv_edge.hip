@@ -71,6 +71,101 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_kernel(
   if (gb < B) out[((size_t)gb * H + y0 + r) * W + x0 + c] = acc;
 }
 
+// Streaming row kernel (64 <= W <= 256, W % 64 == 0; RAW or NORM source): one thread per
+// image column walks down a TH-row band.  Each input row (W pixels x 32 channels) is read
+// ONCE with coalesced float4 loads (next row prefetched into registers), transformed, and
+// staged in LDS (pixel stride 36 floats); each thread then dots its pixel's 32 channels
+// with all 9 taps.  The 9 per-tap partial sums go through an LDS row so every column can
+// gather its three horizontal neighbours; output rows complete one input row later
+// (rolling accumulators).  HBM traffic ~ (TH+2)/TH x the input.
+constexpr int ROWS_TH = 16;
+constexpr int ROWS_PS = 36;   // LDS pixel stride (floats) of the staged row
+
+template <bool NORM, bool FLIP>
+__global__ __launch_bounds__(256) void conv_cout1_rows_kernel(
+    const float* __restrict__ src, const float2* __restrict__ sstats, const float* __restrict__ w,
+    const float* __restrict__ bias, float* __restrict__ out, int H, int W) {
+  constexpr int C = 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int x = threadIdx.x;
+  const int WP = W + 2;
+  // single-buffered: each row's two barriers already separate its writes from the
+  // previous row's reads of P and A
+  float* P = smem;                    // [9][W + 2] per-tap partial sums
+  float* A = smem + 9 * WP;           // [W][ROWS_PS] staged activation row
+  const int nb = H / ROWS_TH;
+  const int b = blockIdx.x / nb, h0 = (blockIdx.x - b * nb) * ROWS_TH;
+  if (x < 18) P[(x / 2) * WP + (x & 1) * (W + 1)] = 0.f;
+  // float4 item k of this thread: row element x + k*W -> pixel (x + k*W) / 8, channels
+  // 4 * (x % 8) .. +3 (W % 8 == 0, so the channel group is the same for every k)
+  const int cq = x & 7;
+  float2 fs[4];
+  if (NORM) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fs[i] = norm_fs(sstats[(size_t)b * C + cq * 4 + i]);
+  }
+  const float* sb = src + (size_t)b * H * W * C;
+  // two rows in flight: r+1 and r+2 are loading while row r is computed
+  float4 nx1[C / 4], nx2[C / 4];
+  auto load_row = [&](int r, float4 (&d)[C / 4]) {
+#pragma unroll
+    for (int k = 0; k < C / 4; ++k)
+      d[k] = (r >= 0 && r < H) ? ld4(sb + (size_t)r * W * C + (size_t)(x + k * W) * 4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const float bb = bias ? bias[0] : 0.f;
+  float acc_m = 0.f, acc_0 = 0.f;   // output rows r-1 and r (row r+1 starts from zero)
+  load_row(h0 - 1, nx1);
+  load_row(h0, nx2);
+  for (int r = h0 - 1; r <= h0 + ROWS_TH; ++r) {
+    float* ab = A;
+    const bool inside = r >= 0 && r < H;
+    float4 cur[C / 4];
+#pragma unroll
+    for (int k = 0; k < C / 4; ++k) { cur[k] = nx1[k]; nx1[k] = nx2[k]; }
+    if (r + 2 <= h0 + ROWS_TH) load_row(r + 2, nx2);
+#pragma unroll
+    for (int k = 0; k < C / 4; ++k) {
+      float4 v = cur[k];
+      if (NORM && inside)
+        v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]), normact_fs(v.z, fs[2]),
+                        normact_fs(v.w, fs[3]));
+      const int e = x + k * W;
+      st4(ab + (e >> 3) * ROWS_PS + cq * 4, v);
+    }
+    __syncthreads();
+    float a[C];
+#pragma unroll
+    for (int q = 0; q < C / 4; ++q) {
+      const float4 v = ld4(ab + x * ROWS_PS + q * 4);
+      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+    }
+    float* pb = P;
+    // channel-major so each channel's 9 weights are adjacent (merged wide scalar loads)
+    float p[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) p[t] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) p[FLIP ? 8 - t : t] = fmaf(a[c], w[c * 9 + t], p[FLIP ? 8 - t : t]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) pb[tap * WP + x + 1] = p[tap];
+    __syncthreads();
+    // input row r feeds output row r+1 with kh = 0, row r with kh = 1, row r-1 with kh = 2
+    float cpart[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const float* row = pb + kh * 3 * WP + x;
+      cpart[kh] = row[0] + row[WP + 1] + row[2 * WP + 2];
+    }
+    const float fin = acc_m + cpart[2];   // output row r-1 is complete
+    if (r - 1 >= h0 && r - 1 < h0 + ROWS_TH) out[((size_t)b * H + r - 1) * W + x] = fin + bb;
+    acc_m = acc_0 + cpart[1];
+    acc_0 = cpart[0];
+  }
+}
+
 // gin[b,h,w,ci] = sum_tap g[b, h-kh+1, w-kw+1] * w[ci][tap]
 template <int CIN>
 __global__ __launch_bounds__(256) void conv_cout1_dgrad_kernel(
@@ -132,6 +227,15 @@ extern "C" int ebsdvae_conv3x3_cout1_fwd(const float* src, const float* src_stat
   EV_REQUIRE(src && w && out && B > 0, "conv3x3_cout1_fwd: null pointer");
   EV_REQUIRE(cin == 32, "conv3x3_cout1_fwd: cin=%d unsupported (32)", cin);
   EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats, "conv3x3_cout1_fwd: NORM needs stats");
+  if ((src_mode == ACT_RAW || src_mode == ACT_NORM) && W >= 64 && W <= 256 && W % 64 == 0 &&
+      H % ROWS_TH == 0) {
+    const size_t lds = ((size_t)9 * (W + 2) + (size_t)W * ROWS_PS) * sizeof(float);
+    auto k = src_mode == ACT_NORM ? (flip ? conv_cout1_rows_kernel<true, true> : conv_cout1_rows_kernel<true, false>)
+                                  : (flip ? conv_cout1_rows_kernel<false, true> : conv_cout1_rows_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3(B * (H / ROWS_TH)), dim3(W), lds, (hipStream_t)stream, src,
+                       (const float2*)src_stats, w, bias, out, H, W);
+    return evh::check_launch("conv3x3_cout1_fwd");
+  }
   EV_REQUIRE(edge_geom(H, W, &g), "conv3x3_cout1_fwd: unsupported shape %dx%d", H, W);
   const int tiles = ((B + g.NI - 1) / g.NI) * (H / g.TH) * (W / g.TW);
   const size_t lds = (size_t)g.NI * (g.TH + 2) * (g.TW + 2) * 33 * sizeof(float);

@@ -462,6 +462,33 @@ __global__ void pack_conv_weight_kernel(const float* __restrict__ s, float* __re
   }
 }
 
+struct PackBatch {
+  ebsdvae_pack_desc d[EBSDVAE_MAX_PACK];
+};
+
+// one launch packs every conv weight of a step: blockIdx.y = descriptor (kernel argument)
+__global__ void pack_conv_weights_kernel(const PackBatch pb) {
+  const ebsdvae_pack_desc& q = pb.d[blockIdx.y];
+  const int ci_ = q.for_dgrad ? q.cout : q.cin;
+  const int co_ = q.for_dgrad ? q.cin : q.cout;
+  const int ck = ci_ < CK ? ci_ : CK;
+  const int n = 9 * ci_ * co_;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int o = e % co_;
+    const int r = e / co_;
+    const int c8 = r % ck;
+    const int r2 = r / ck;
+    const int t = r2 % 9, chunk = r2 / 9;
+    const int i = chunk * ck + c8;
+    const int co = q.for_dgrad ? i : o;
+    const int ci = q.for_dgrad ? o : i;
+    size_t idx;
+    if (q.kind == 0) idx = ((size_t)co * q.cin + ci) * 9 + (q.for_dgrad ? 8 - t : t);
+    else idx = ((size_t)ci * q.cout + co) * 9 + (q.for_dgrad ? t : 8 - t);
+    q.dst[e] = q.src[idx];
+  }
+}
+
 // ------------------------------------------------------------------ host-side planning
 struct Cfg {
   int kind;   // 0 big, 1 small, 2 cin1
@@ -592,6 +619,25 @@ extern "C" int ebsdvae_pack_conv_weight(const float* src, float* dst, int cin, i
   hipLaunchKernelGGL(pack_conv_weight_kernel, dim3(blocks < 1024 ? blocks : 1024), dim3(256), 0,
                      (hipStream_t)stream, src, dst, cin, cout, kind, for_dgrad);
   return evh::check_launch("pack_conv_weight");
+}
+
+extern "C" int ebsdvae_pack_conv_weights(const ebsdvae_pack_desc* descs, int n,
+                                         ebsdvae_stream_t stream) {
+  EV_REQUIRE(descs && n > 0 && n <= EBSDVAE_MAX_PACK, "pack_conv_weights: n=%d out of range", n);
+  PackBatch pb;
+  int maxn = 0;
+  for (int i = 0; i < n; ++i) {
+    const ebsdvae_pack_desc& q = descs[i];
+    EV_REQUIRE(q.src && q.dst && q.cin > 0 && q.cout > 0 && (q.kind == 0 || q.kind == 1),
+               "pack_conv_weights: bad descriptor %d", i);
+    pb.d[i] = q;
+    const int e = 9 * q.cin * q.cout;
+    if (e > maxn) maxn = e;
+  }
+  int bx = (maxn + 255) / 256;
+  if (bx > 64) bx = 64;
+  hipLaunchKernelGGL(pack_conv_weights_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, pb);
+  return evh::check_launch("pack_conv_weights");
 }
 
 extern "C" int ebsdvae_conv3x3_fwd(const float* src, const float* src_stats, int src_mode,

@@ -5,18 +5,23 @@
 //   std    = exp(logvar / 2) ;  z = mu + eps * std                (Normal(mu,std).rsample)
 //   dec_in = (z @ W2^T + b2).view(B, C, S, S)   -> written NHWC for the decoder
 //
-// One workgroup per pattern: the F-wide feature row lives in LDS, the two F->L heads are
-// wave-per-output dot products with coalesced weight rows and wave64 shuffle reductions.
-// The NCHW<->NHWC flatten permutation is folded into the LDS index, so the NHWC encoder
-// output never needs a transpose pass.
+// One 1024-thread workgroup per pattern (16 waves: the heads sit on the critical path
+// between encoder and decoder, so latency matters more than the tiny FLOP count): the
+// F-wide feature row lives in LDS, each thread dots its k-slice against every head row
+// (coalesced weight rows), and the per-output sums fold through wave shuffles + LDS in a
+// fixed order.  The NCHW<->NHWC flatten permutation is folded into the LDS index, so the
+// NHWC encoder output never needs a transpose pass.
 #include "common.h"
 #include "../../include/ebsdvae.h"
 
 namespace ev {
 
 constexpr int MAXL = 64;
+constexpr int HT = 1024;         // threads per pattern
+constexpr int HW_ = HT / 64;     // waves per pattern
+constexpr int OCH = 32;          // head outputs per register chunk
 
-__global__ __launch_bounds__(256) void heads_fwd_kernel(
+__global__ __launch_bounds__(HT) void heads_fwd_kernel(
     const float* __restrict__ enc, const float* __restrict__ wmu, const float* __restrict__ bmu,
     const float* __restrict__ wlv, const float* __restrict__ blv, const float* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ eps, float* __restrict__ flat,
@@ -24,28 +29,42 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(
     float* __restrict__ dec, int C, int S, int L) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int F = C * S * S;
-  float* f = sm;           // [F]
-  float* lat = sm + F;     // [2L]
-  float* zs = lat + 2 * MAXL;
+  float* f = sm;                  // [F]
+  float* red = sm + F;            // [HW_][2 * MAXL]
+  float* zs = red + HW_ * 2 * MAXL;   // [MAXL]
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* e = enc + (size_t)b * F;
-  for (int i = tid; i < F; i += 256) {   // i = NHWC index within the pattern
+  for (int i = tid; i < F; i += HT) {   // i = NHWC index within the pattern
     const int c = i % C, hw = i / C;
-    const float v = e[i];
-    f[c * S * S + hw] = v;
+    f[c * S * S + hw] = e[i];
   }
   __syncthreads();
-  for (int k = tid; k < F; k += 256) flat[(size_t)b * F + k] = f[k];
-  for (int o = wave; o < 2 * L; o += 4) {
-    const float* wr = (o < L) ? (wmu + (size_t)o * F) : (wlv + (size_t)(o - L) * F);
-    float s = 0.f;
-    for (int k = lane; k < F; k += 64) s = fmaf(f[k], wr[k], s);
-    s = wave_sum(s);
-    if (lane == 0) lat[o] = s + ((o < L) ? bmu[o] : blv[o - L]);
+  for (int k = tid; k < F; k += HT) flat[(size_t)b * F + k] = f[k];
+  for (int o0 = 0; o0 < 2 * L; o0 += OCH) {
+    float acc[OCH];
+#pragma unroll
+    for (int j = 0; j < OCH; ++j) acc[j] = 0.f;
+    for (int k = tid; k < F; k += HT) {
+      const float fk = f[k];
+#pragma unroll
+      for (int j = 0; j < OCH; ++j) {
+        const int o = o0 + j;
+        if (o < 2 * L) acc[j] = fmaf(fk, (o < L) ? wmu[(size_t)o * F + k] : wlv[(size_t)(o - L) * F + k], acc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < OCH; ++j) {
+      const float v = wave_sum(acc[j]);
+      if (lane == 0 && o0 + j < 2 * L) red[wave * 2 * MAXL + o0 + j] = v;
+    }
   }
   __syncthreads();
   if (tid < L) {
-    const float m = lat[tid], lv = lat[L + tid];
+    float m = bmu[tid], lv = blv[tid];
+    for (int w = 0; w < HW_; ++w) {
+      m += red[w * 2 * MAXL + tid];
+      lv += red[w * 2 * MAXL + L + tid];
+    }
     const float sd = expf(lv * 0.5f);
     const float zz = fmaf(eps[(size_t)b * L + tid], sd, m);
     mu[(size_t)b * L + tid] = m;
@@ -54,7 +73,7 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(
     zs[tid] = zz;
   }
   __syncthreads();
-  for (int o = tid; o < F; o += 256) {
+  for (int o = tid; o < F; o += HT) {
     const float* wr = w2 + (size_t)o * L;
     float s = b2[o];
     for (int j = 0; j < L; ++j) s = fmaf(wr[j], zs[j], s);
@@ -64,47 +83,47 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(
 }
 
 // gs layout per pattern: [g_mu_tot (L) | g_logvar (L) | g_out (F)]
-__global__ __launch_bounds__(256) void heads_bwd_kernel(
+__global__ __launch_bounds__(HT) void heads_bwd_kernel(
     const float* __restrict__ gdec, const float* __restrict__ gz, const float* __restrict__ gmu,
     const float* __restrict__ gstd, const float* __restrict__ stdv, const float* __restrict__ eps,
     const float* __restrict__ wmu, const float* __restrict__ wlv, const float* __restrict__ w2,
     float* __restrict__ genc, float* __restrict__ gs, int C, int S, int L) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int F = C * S * S;
-  float* go = sm;               // [F] g_out in flat (NCHW) order
-  float* red = sm + F;          // [4][MAXL]
-  float* gl = red + 4 * MAXL;   // [2L]: g_mu_tot, g_logvar
+  float* go = sm;                   // [F] g_out in flat (NCHW) order
+  float* red = sm + F;              // [HW_][MAXL]
+  float* gl = red + HW_ * MAXL;     // [2L]: g_mu_tot, g_logvar
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* gsb = gs + (size_t)b * (2 * L + F);
-  for (int i = tid; i < F; i += 256) {
+  for (int i = tid; i < F; i += HT) {
     const int c = i % C, hw = i / C;
     go[c * S * S + hw] = gdec[(size_t)b * F + i];
   }
   __syncthreads();
-  float acc[MAXL];
+  for (int o = tid; o < F; o += HT) gsb[2 * L + o] = go[o];
+  for (int j0 = 0; j0 < L; j0 += 16) {   // g_z[j] = sum_o g_out[o] * W2[o][j]
+    float acc[16];
 #pragma unroll
-  for (int j = 0; j < MAXL; ++j) acc[j] = 0.f;
-  for (int o = tid; o < F; o += 256) {
-    const float g = go[o];
-    gsb[2 * L + o] = g;
-    const float* wr = w2 + (size_t)o * L;
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    for (int o = tid; o < F; o += HT) {
+      const float g = go[o];
+      const float* wr = w2 + (size_t)o * L + j0;
 #pragma unroll
-    for (int j = 0; j < MAXL; ++j)
-      if (j < L) acc[j] = fmaf(g, wr[j], acc[j]);
-  }
+      for (int j = 0; j < 16; ++j)
+        if (j0 + j < L) acc[j] = fmaf(g, wr[j], acc[j]);
+    }
 #pragma unroll
-  for (int j = 0; j < MAXL; ++j) {
-    if (j < L) {
+    for (int j = 0; j < 16; ++j) {
       const float v = wave_sum(acc[j]);
-      if (lane == 0) red[wave * MAXL + j] = v;
+      if (lane == 0 && j0 + j < L) red[wave * MAXL + j0 + j] = v;
     }
   }
   __syncthreads();
   if (tid < L) {
     const int j = tid;
     const size_t bj = (size_t)b * L + j;
-    const float gzt = red[j] + red[MAXL + j] + red[2 * MAXL + j] + red[3 * MAXL + j] +
-                      (gz ? gz[bj] : 0.f);
+    float gzt = gz ? gz[bj] : 0.f;
+    for (int w = 0; w < HW_; ++w) gzt += red[w * MAXL + j];
     const float sd = stdv[bj];
     const float gmt = gzt + (gmu ? gmu[bj] : 0.f);
     const float glv = ((gstd ? gstd[bj] : 0.f) + gzt * eps[bj]) * sd * 0.5f;
@@ -114,7 +133,7 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     gsb[L + j] = glv;
   }
   __syncthreads();
-  for (int k = tid; k < F; k += 256) {
+  for (int k = tid; k < F; k += HT) {
     float s = 0.f;
     for (int j = 0; j < L; ++j) {
       s = fmaf(gl[j], wmu[(size_t)j * F + k], s);
@@ -125,42 +144,74 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
   }
 }
 
-// weight grads of the three Linear layers: batch reduction in fixed order.
-// thread e < F: dWmu[:,e], dWlv[:,e] (k-role) and dW2[e,:], db2[e] (o-role);
-// threads F..F+L-1: dbmu, dblv.
+// Weight grads of the three Linear layers as a split-batch reduction: blockIdx.y takes a
+// chunk of HB patterns; thread (j, e) (e fastest: coalesced flat / g_out rows) writes its
+// chunk's partial dWmu[j][e], dWlv[j][e], dW2[e][j] (stored [j][e]) and, for j == 0,
+// db2[e]; threads past F*L take dbmu / dblv.  heads_wgrad_reduce sums the chunks in order.
+constexpr int HB = 16;   // patterns per chunk
+
 __global__ __launch_bounds__(256) void heads_wgrad_kernel(
     const float* __restrict__ flat, const float* __restrict__ z, const float* __restrict__ gs,
-    float* __restrict__ gwmu, float* __restrict__ gbmu, float* __restrict__ gwlv,
-    float* __restrict__ gblv, float* __restrict__ gw2, float* __restrict__ gb2, int B, int F, int L) {
-  // thread (j, e): e fastest (coalesced flat / g_out rows), j = latent index
+    float* __restrict__ part, int B, int F, int L) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int G = 2 * L + F;
+  const size_t FL = (size_t)F * L;
+  const size_t per = 3 * FL + F + 2 * L;   // one chunk's partial record
+  float* pc = part + (size_t)blockIdx.y * per;
+  const int b0 = blockIdx.y * HB, b1 = min(b0 + HB, B);
   if (idx < F * L) {
     const int j = idx / F, e = idx - j * F;
     float am = 0.f, al = 0.f, a2 = 0.f, ab = 0.f;
-    for (int b = 0; b < B; ++b) {
+#pragma unroll 4
+    for (int b = b0; b < b1; ++b) {
       const float fv = flat[(size_t)b * F + e];
-      const float go = gs[(size_t)b * G + 2 * L + e];
       const float* gb = gs + (size_t)b * G;
+      const float go = gb[2 * L + e];
       am = fmaf(gb[j], fv, am);
       al = fmaf(gb[L + j], fv, al);
       a2 = fmaf(go, z[(size_t)b * L + j], a2);
       ab += go;
     }
-    gwmu[(size_t)j * F + e] = am;
-    gwlv[(size_t)j * F + e] = al;
-    gw2[(size_t)e * L + j] = a2;
-    if (j == 0) gb2[e] = ab;
+    pc[idx] = am;
+    pc[FL + idx] = al;
+    pc[2 * FL + idx] = a2;
+    if (j == 0) pc[3 * FL + e] = ab;
   } else if (idx < F * L + L) {
-    const int e = idx - F * L + F;
-    const int j = e - F;
+    const int j = idx - F * L;
     float sm = 0.f, sl = 0.f;
-    for (int b = 0; b < B; ++b) {
+    for (int b = b0; b < b1; ++b) {
       sm += gs[(size_t)b * G + j];
       sl += gs[(size_t)b * G + L + j];
     }
-    gbmu[j] = sm;
-    gblv[j] = sl;
+    pc[3 * FL + F + j] = sm;
+    pc[3 * FL + F + L + j] = sl;
+  }
+}
+
+__global__ __launch_bounds__(256) void heads_wgrad_reduce_kernel(
+    const float* __restrict__ part, int nch, float* __restrict__ gwmu, float* __restrict__ gbmu,
+    float* __restrict__ gwlv, float* __restrict__ gblv, float* __restrict__ gw2,
+    float* __restrict__ gb2, int F, int L) {
+  const size_t FL = (size_t)F * L;
+  const size_t per = 3 * FL + F + 2 * L;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= per) return;
+  float s = 0.f;
+  for (int c = 0; c < nch; ++c) s += part[(size_t)c * per + i];
+  if (i < FL) {
+    gwmu[i] = s;
+  } else if (i < 2 * FL) {
+    gwlv[i - FL] = s;
+  } else if (i < 3 * FL) {
+    const size_t r = i - 2 * FL;           // [j][e] -> W2 grad layout [e][j]
+    const size_t j = r / F, e = r - j * F;
+    gw2[e * L + j] = s;
+  } else if (i < 3 * FL + F) {
+    gb2[i - 3 * FL] = s;
+  } else if (i < 3 * FL + F + L) {
+    gbmu[i - 3 * FL - F] = s;
+  } else {
+    gblv[i - 3 * FL - F - L] = s;
   }
 }
 
@@ -276,9 +327,14 @@ extern "C" int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const floa
              "heads_fwd: null pointer");
   EV_REQUIRE(B > 0 && L > 0 && L <= MAXL && C > 0 && S > 0, "heads_fwd: bad shape L=%d", L);
   const int F = C * S * S;
-  const size_t lds = (F + 3 * MAXL) * sizeof(float);
+  const size_t lds = (F + (HW_ * 2 + 1) * MAXL) * sizeof(float);
   EV_REQUIRE(lds <= 160 * 1024, "heads_fwd: feature width %d too large", F);
-  hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, enc, w_mu, b_mu,
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)heads_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(HT), lds, (hipStream_t)stream, enc, w_mu, b_mu,
                      w_lv, b_lv, w_l2, b_l2, eps, flat, mu, std, z, dec_in, C, S, L);
   return evh::check_launch("heads_fwd");
 }
@@ -291,22 +347,38 @@ extern "C" int ebsdvae_heads_bwd(const float* g_dec, const float* g_z, const flo
   EV_REQUIRE(g_dec && std && eps && w_mu && w_lv && w_l2 && g_enc && gs, "heads_bwd: null pointer");
   EV_REQUIRE(B > 0 && L > 0 && L <= MAXL, "heads_bwd: bad shape");
   const int F = C * S * S;
-  const size_t lds = (F + 6 * MAXL) * sizeof(float);
+  const size_t lds = (F + (HW_ + 2) * MAXL) * sizeof(float);
   EV_REQUIRE(lds <= 160 * 1024, "heads_bwd: feature width too large");
-  hipLaunchKernelGGL(heads_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, g_dec, g_z, g_mu,
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)heads_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(heads_bwd_kernel, dim3(B), dim3(HT), lds, (hipStream_t)stream, g_dec, g_z, g_mu,
                      g_std, std, eps, w_mu, w_lv, w_l2, g_enc, gs, C, S, L);
   return evh::check_launch("heads_bwd");
 }
 
+extern "C" size_t ebsdvae_heads_wgrad_work(int B, int F, int L) {
+  const size_t per = 3 * (size_t)F * L + F + 2 * (size_t)L;
+  return (size_t)((B + HB - 1) / HB) * per * sizeof(float);
+}
+
 extern "C" int ebsdvae_heads_wgrad(const float* flat, const float* z, const float* gs, float* gw_mu,
                                    float* gb_mu, float* gw_lv, float* gb_lv, float* gw_l2,
-                                   float* gb_l2, int B, int F, int L, ebsdvae_stream_t stream) {
-  EV_REQUIRE(flat && z && gs && gw_mu && gb_mu && gw_lv && gb_lv && gw_l2 && gb_l2,
+                                   float* gb_l2, void* work, int B, int F, int L,
+                                   ebsdvae_stream_t stream) {
+  EV_REQUIRE(flat && z && gs && gw_mu && gb_mu && gw_lv && gb_lv && gw_l2 && gb_l2 && work,
              "heads_wgrad: null pointer");
-  EV_REQUIRE(L > 0 && L <= MAXL, "heads_wgrad: bad L");
+  EV_REQUIRE(B > 0 && L > 0 && L <= MAXL, "heads_wgrad: bad L");
   const int n = F * L + L;
-  hipLaunchKernelGGL(heads_wgrad_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     flat, z, gs, gw_mu, gb_mu, gw_lv, gb_lv, gw_l2, gb_l2, B, F, L);
+  const int nch = (B + HB - 1) / HB;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(heads_wgrad_kernel, dim3((n + 255) / 256, nch), dim3(256), 0, s, flat, z, gs,
+                     (float*)work, B, F, L);
+  const size_t per = 3 * (size_t)F * L + F + 2 * (size_t)L;
+  hipLaunchKernelGGL(heads_wgrad_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s,
+                     (const float*)work, nch, gw_mu, gb_mu, gw_lv, gb_lv, gw_l2, gb_l2, F, L);
   return evh::check_launch("heads_wgrad");
 }
 

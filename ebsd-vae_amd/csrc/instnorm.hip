@@ -231,18 +231,32 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
   }
 }
 
-__global__ void in_bwd_finalize_kernel(const double2* __restrict__ part, float2* __restrict__ bst,
-                                       int B, int C, int T, double inv_hw) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= B * C) return;
-  const int b = e / C, c = e - b * C;
+// One workgroup per pattern b (C <= 256): thread (c = tid % C, j = tid / C) sums tiles
+// j, j+J, ... of channel c in double, then lane j == 0 folds the J sums in order.
+__global__ __launch_bounds__(256) void in_bwd_finalize_kernel(const double2* __restrict__ part,
+                                                              float2* __restrict__ bst, int C,
+                                                              int T, double inv_hw) {
+  __shared__ double sm[2][256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int J = 256 / C;
+  const int c = tid % C, j = tid / C;
+  const double2* p = part + (size_t)b * T * C + c;
   double s1 = 0.0, s2 = 0.0;
-  for (int t = 0; t < T; ++t) {
-    const double2 v = part[((size_t)b * T + t) * C + c];
-    s1 += v.x;
-    s2 += v.y;
+  if (j < J) {
+    for (int t = j; t < T; t += J) {
+      const double2 v = p[(size_t)t * C];
+      s1 += v.x;
+      s2 += v.y;
+    }
   }
-  bst[e] = make_float2((float)(s1 * inv_hw), (float)(s2 * inv_hw));
+  sm[0][tid] = s1;
+  sm[1][tid] = s2;
+  __syncthreads();
+  if (j == 0) {
+    double a = 0.0, q = 0.0;
+    for (int k = 0; k < J; ++k) { a += sm[0][k * C + c]; q += sm[1][k * C + c]; }
+    bst[(size_t)b * C + c] = make_float2((float)(a * inv_hw), (float)(q * inv_hw));
+  }
 }
 
 // ------------------------------------------------------------------ network-end fusions
@@ -483,10 +497,9 @@ extern "C" int ebsdvae_in_bwd_reduce(const float* gnext, int pmode, const float*
 extern "C" int ebsdvae_in_bwd_finalize(const double* part, float* bstats, int B, int C, int tiles,
                                        int HW, ebsdvae_stream_t stream) {
   EV_REQUIRE(part && bstats, "in_bwd_finalize: null pointer");
-  const int n = B * C;
-  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, (const double2*)part, (float2*)bstats, B, C, tiles,
-                     1.0 / (double)HW);
+  EV_REQUIRE(C > 0 && C <= 256 && 256 % C == 0 && tiles > 0, "in_bwd_finalize: C=%d unsupported", C);
+  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream,
+                     (const double2*)part, (float2*)bstats, C, tiles, 1.0 / (double)HW);
   return evh::check_launch("in_bwd_finalize");
 }
 

@@ -26,6 +26,7 @@ SIGNATURES = {
     "ebsdvae_last_error": [],
     "ebsdvae_version": [],
     "ebsdvae_pack_conv_weight": [P, P, I, I, I, I, P],
+    "ebsdvae_pack_conv_weights": [P, I, P],
     "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_stat_tiles": [I, I, I],
     "ebsdvae_conv3x3_dgrad_inbwd": [P, P, P, P, P, I, P, I, I, I, I, I, P],
@@ -47,7 +48,8 @@ SIGNATURES = {
     "ebsdvae_in_bwd_first_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
-    "ebsdvae_heads_wgrad": [P, P, P, P, P, P, P, P, P, I, I, I, P],
+    "ebsdvae_heads_wgrad_work": [I, I, I],
+    "ebsdvae_heads_wgrad": [P, P, P, P, P, P, P, P, P, P, I, I, I, P],
     "ebsdvae_linear_fwd": [P, P, P, P, I, I, I, P],
     "ebsdvae_linear_bwd": [P, P, P, P, P, P, I, I, I, P],
     "ebsdvae_reparam_fwd": [P, P, P, P, P, I64, P],
@@ -57,13 +59,23 @@ SIGNATURES = {
     "ebsdvae_vae_loss_bwd": [P, P, P, P, P, F, P, P, P, P, F, P, P, P, P, P, I, I, I, P],
     "ebsdvae_adam": [P, P, P, P, P, P, I64, F, F, F, F, F, I, P],
 }
-_RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t}
+_RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t,
+            "ebsdvae_heads_wgrad_work": ctypes.c_size_t}
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
-           "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work"}
+           "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work"}
 
 _lib = None
 _lock = threading.Lock()
+
+
+class PackDesc(ctypes.Structure):
+    """ebsdvae_pack_desc (include/ebsdvae.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("cin", ctypes.c_int),
+                ("cout", ctypes.c_int), ("kind", ctypes.c_int), ("for_dgrad", ctypes.c_int)]
+
+
+MAX_PACK = 64
 
 
 class NativeLibraryError(RuntimeError):

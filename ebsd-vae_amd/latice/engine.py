@@ -18,6 +18,7 @@ from the PyTorch caching allocator and every launch goes to the current HIP stre
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field
 
 import torch
@@ -166,12 +167,44 @@ def pack_weight(w, layer: ConvLayer, dgrad: bool):
     return out
 
 
-def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False):
+class PackSet:
+    """Packed forward / input-gradient weights of every conv layer of a plan, refreshed by
+    ONE batched launch (ebsdvae_pack_conv_weights) per step.  The parameter tensors must
+    keep their storage (e.g. views into the trainer's flat buffer)."""
+
+    def __init__(self, plan: "Plan", params):
+        self.packs = {}
+        descs = []
+        for i, L in enumerate(plan.enc):
+            self._add(L, params[L.name + ".weight"], dgrad=i > 0, descs=descs)
+        for L in plan.dec:
+            self._add(L, params[L.name + ".weight"], dgrad=True, descs=descs)
+        if len(descs) > N.MAX_PACK:
+            raise RuntimeError(f"PackSet: {len(descs)} packs > {N.MAX_PACK}")
+        self.n = len(descs)
+        self.descs = (N.PackDesc * self.n)(*descs)
+
+    def _add(self, L, w, dgrad, descs):
+        pf = _empty(9 * L.cin * L.cout, like=w)
+        descs.append(N.PackDesc(N.ptr(w), N.ptr(pf), L.cin, L.cout, L.kind, 0))
+        pd = None
+        if dgrad:
+            pd = _empty(9 * L.cin * L.cout, like=w)
+            descs.append(N.PackDesc(N.ptr(w), N.ptr(pd), L.cin, L.cout, L.kind, 1))
+        self.packs[L.name] = (pf, pd)
+
+    def refresh(self):
+        N.call("ebsdvae_pack_conv_weights", ctypes.addressof(self.descs), self.n, N.stream())
+        return self.packs
+
+
+def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=None):
     """One conv block forward: y (B,H,H,cout) pre-norm + IN stats {mean,rstd} (B,cout,2).
     keep_act: also return the conv's logical input (materialised by the kernel), used by
-    max-pool-fed layers so their wgrad reads the pooled tensor."""
+    max-pool-fed layers so their wgrad reads the pooled tensor.  wp: pre-packed weight."""
     H = layer.H
-    wp = pack_weight(w, layer, dgrad=False)
+    if wp is None:
+        wp = pack_weight(w, layer, dgrad=False)
     y = _empty(B, H, H, layer.cout, like=w)
     T = N.call("ebsdvae_conv3x3_stat_tiles", H, H, layer.cout)
     part = _empty(B, T, layer.cout, 2, like=w)
@@ -278,12 +311,13 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
            cin, cout, kind, work.data_ptr(), s)
 
 
-def conv_dgrad(gy, layer: ConvLayer, w, prev=None):
+def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None):
     """Input gradient of `layer`.  prev = (y_prev, st_prev, pmode_prev) of the block feeding
     it: the previous block's InstanceNorm-backward reduce is then fused into the epilogue and
     (gin, part) is returned for in_backward(..., part=part)."""
     B, H, W, _ = gy.shape
-    wd = pack_weight(w, layer, dgrad=True)
+    if wd is None:
+        wd = pack_weight(w, layer, dgrad=True)
     gin = _empty(B, H, W, layer.cin, like=gy)
     tag = f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}"
     flops = conv_flops(B, H, W, layer.cin, layer.cout)
@@ -308,18 +342,24 @@ def _grad_buf(grads, name, like):
 
 
 # ----------------------------------------------------------------------------- encoder
-def encoder_forward(plan: Plan, x, params):
-    """x: (B,1,S,S) fp32 (== NHWC).  Returns (enc_out NHWC (B,s,s,C), saved)."""
+def _wp(packs, name, k):
+    return None if packs is None else packs[name][k]
+
+
+def encoder_forward(plan: Plan, x, params, packs=None):
+    """x: (B,1,S,S) fp32 (== NHWC).  Returns (enc_out NHWC (B,s,s,C), saved).
+    packs: PackSet.refresh() result (None: pack each weight on the fly)."""
     B = x.shape[0]
     saved = {}
     src, sst = x, None
     for L in plan.enc:
         w, b = params[L.name + ".weight"], params[L.name + ".bias"]
+        wp = _wp(packs, L.name, 0)
         if L.src_mode == ACT_NORM_POOL:
-            y, st, act = conv_forward(src, sst, L, w, b, B, keep_act=True)
+            y, st, act = conv_forward(src, sst, L, w, b, B, keep_act=True, wp=wp)
             saved[L.name + ".act_in"] = act
         else:
-            y, st = conv_forward(src, sst, L, w, b, B)
+            y, st = conv_forward(src, sst, L, w, b, B, wp=wp)
         saved[L.name] = (y, st)
         src, sst = y, st
     s, C = plan.enc_side, plan.enc_channels
@@ -329,7 +369,7 @@ def encoder_forward(plan: Plan, x, params):
     return out, saved
 
 
-def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=False):
+def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=False, packs=None):
     """g_enc: grad of the encoder output (B,s,s,C) NHWC.  Returns (grads dict, gx or None)."""
     out = {}
     g_next, part = g_enc, None
@@ -360,7 +400,8 @@ def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=Fa
         out[wn], out[bn] = dw, db
         if i > 0:
             P = plan.enc[i - 1]
-            g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode))
+            g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode),
+                                      wd=_wp(packs, L.name, 1))
         elif need_gx:
             B, H, W, _ = gy.shape
             gx = _empty(B, 1, H, W, like=gy)
@@ -398,19 +439,22 @@ def heads_backward(plan: Plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, param
            N.ptr(eps), N.ptr(params["mu.0.weight"]), N.ptr(params["logvar.0.weight"]),
            N.ptr(params["linear2.0.weight"]), N.ptr(g_enc), N.ptr(gs), B, C, s, L, N.stream())
     out = {n: _grad_buf(grads, n, params[n]) for n in HEAD_NAMES}
+    nbytes = N.call("ebsdvae_heads_wgrad_work", B, F, L)
+    work = torch.empty(nbytes // 4, dtype=torch.float32, device=g_dec.device)
     N.call("ebsdvae_heads_wgrad", N.ptr(flat), N.ptr(z), N.ptr(gs),
-           *[N.ptr(out[n]) for n in HEAD_NAMES], B, F, L, N.stream())
+           *[N.ptr(out[n]) for n in HEAD_NAMES], N.ptr(work), B, F, L, N.stream())
     return g_enc, out
 
 
 # ----------------------------------------------------------------------------- decoder
-def decoder_forward(plan: Plan, dec_in, params):
+def decoder_forward(plan: Plan, dec_in, params, packs=None):
     """dec_in: (B,s,s,C) NHWC.  Returns (x_hat (B,1,S,S), saved)."""
     B = dec_in.shape[0]
     saved = {"__dec_in__": dec_in}
     src, sst = dec_in, None
     for L in plan.dec:
-        y, st = conv_forward(src, sst, L, params[L.name + ".weight"], params[L.name + ".bias"], B)
+        y, st = conv_forward(src, sst, L, params[L.name + ".weight"], params[L.name + ".bias"], B,
+                             wp=_wp(packs, L.name, 0))
         saved[L.name] = (y, st)
         src, sst = y, st
     S = plan.image_size
@@ -421,7 +465,7 @@ def decoder_forward(plan: Plan, dec_in, params):
     return x_hat, saved
 
 
-def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None):
+def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None, packs=None):
     """g_xhat: (B,1,S,S).  Returns (grads dict, g_dec_in (B,s,s,C) NHWC)."""
     out = {}
     B = g_xhat.shape[0]
@@ -449,9 +493,10 @@ def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None):
         out[wn], out[bn] = dw, db
         if i > 0:
             P = plan.dec[i - 1]
-            g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode))
+            g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode),
+                                      wd=_wp(packs, L.name, 1))
         else:
-            g_next = conv_dgrad(gy, L, params[wn])
+            g_next = conv_dgrad(gy, L, params[wn], wd=_wp(packs, L.name, 1))
     s, C = plan.enc_side, plan.enc_channels
     g_dec = _empty(B, s, s, C, like=g_xhat)
     N.call("ebsdvae_upsample2_bwd", N.ptr(g_next), N.ptr(g_dec), B, s, s, C, N.stream())

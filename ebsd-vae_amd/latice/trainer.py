@@ -99,6 +99,7 @@ class VAETrainer:
         self._eps = None
         self.graph = None
         self._static = None
+        self.packset = E.PackSet(self.plan, self.P)   # params are views of self.flat
 
     @property
     def numel(self) -> int:
@@ -114,17 +115,18 @@ class VAETrainer:
         """fwd + loss + bwd into self.gflat (+ the DP gradient exchange).  Returns the three
         loss scalars (device tensors)."""
         plan, P, G = self.plan, self.P, self.G
-        enc, se = E.encoder_forward(plan, x, P)
+        packs = self.packset.refresh()   # one launch packs every conv weight of the step
+        enc, se = E.encoder_forward(plan, x, P, packs=packs)
         eps = self._noise(x.shape[0]) if eps is None else eps
         flat, mu, std, z, dec_in = E.heads_forward(plan, enc, P, eps)
-        x_hat, sd = E.decoder_forward(plan, dec_in, P)
+        x_hat, sd = E.decoder_forward(plan, dec_in, P, packs=packs)
         (loss, kl, rec), _ = E.loss_forward(x_hat, x, z, mu, std, self.kl_lambda)
         g_xhat, g_z, g_mu, g_std, _ = E.loss_backward(x_hat, x, z, mu, std, self.kl_lambda,
                                                       g_loss=self.one, scale=1.0 / self.world)
-        _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G)
+        _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
         g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P, grads=G)
         self.reducer.start(0)
-        E.encoder_backward(plan, g_enc, x, se, P, grads=G)
+        E.encoder_backward(plan, g_enc, x, se, P, grads=G, packs=packs)
         self.reducer.start(1)
         self.reducer.finish()
         return loss, kl, rec

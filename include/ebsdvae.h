@@ -46,6 +46,16 @@ int ebsdvae_version(void);
 int ebsdvae_pack_conv_weight(const float* src, float* dst, int cin, int cout, int kind,
                              int for_dgrad, ebsdvae_stream_t stream);
 
+/* Batched form: n <= EBSDVAE_MAX_PACK descriptors in HOST memory (passed to the kernel by
+ * value), one launch for every conv weight of a step. */
+#define EBSDVAE_MAX_PACK 64
+typedef struct {
+  const float* src; /* device */
+  float* dst;       /* device */
+  int cin, cout, kind, for_dgrad;
+} ebsdvae_pack_desc;
+int ebsdvae_pack_conv_weights(const ebsdvae_pack_desc* descs, int n, ebsdvae_stream_t stream);
+
 /* ---- 3x3 conv, implicit GEMM on fp32 MFMA -------------------------------------------
  * y[b,h,w,co] = bias[co] + sum_{tap,ci} act(src)[b,h+dh,w+dw,ci] * wpack[tap][ci][co]
  * (zero padding 1).  Replaces nn.Conv2d / nn.ConvTranspose2d forward
@@ -166,9 +176,14 @@ int ebsdvae_heads_bwd(const float* g_dec, const float* g_z, const float* g_mu,
                       const float* g_std, const float* std, const float* eps,
                       const float* w_mu, const float* w_lv, const float* w_l2, float* g_enc,
                       float* gs, int B, int C, int S, int L, ebsdvae_stream_t stream);
+/* Weight/bias gradients of the three Linear heads (autograd's addmm backward for
+ * latice/model.py:127-131): deterministic split-batch reduction through `work`
+ * (ebsdvae_heads_wgrad_work(B,F,L) bytes, caller-owned). */
+size_t ebsdvae_heads_wgrad_work(int B, int F, int L);
 int ebsdvae_heads_wgrad(const float* flat, const float* z, const float* gs, float* gw_mu,
                         float* gb_mu, float* gw_lv, float* gb_lv, float* gw_l2,
-                        float* gb_l2, int B, int F, int L, ebsdvae_stream_t stream);
+                        float* gb_l2, void* work, int B, int F, int L,
+                        ebsdvae_stream_t stream);
 
 /* generic Linear (y = x W^T + b), for direct calls of model.mu / .logvar / .linear2 */
 int ebsdvae_linear_fwd(const float* x, const float* w, const float* b, float* y, int M,

@@ -378,3 +378,21 @@ def test_fused_first_conv_weight_grad(cuda):
     rw, rb = O.conv3x3_wgrad(x, gy)
     assert O.rel_err(host(dw), rw) < 1e-4
     assert np.abs(host(db) - rb).max() < 1e-4 * max(1.0, np.abs(rb).max())
+
+
+def test_batched_weight_pack_matches_single_packs(cuda):
+    """ebsdvae_pack_conv_weights (one launch per step) == per-layer ebsdvae_pack_conv_weight."""
+    plan = E.build_plan(32, 16, 128)
+    rng = np.random.default_rng(17)
+    params = {}
+    for L in plan.enc + plan.dec:
+        shape = (L.cout, L.cin, 3, 3) if L.kind == E.KIND_CONV else (L.cin, L.cout, 3, 3)
+        params[L.name + ".weight"] = dev(rng.standard_normal(shape))
+    ps = E.PackSet(plan, params)
+    packs = ps.refresh()
+    for i, L in enumerate(plan.enc + plan.dec):
+        w = params[L.name + ".weight"]
+        pf, pd = packs[L.name]
+        assert torch.equal(pf, E.pack_weight(w, L, dgrad=False)), L.name
+        if pd is not None:
+            assert torch.equal(pd, E.pack_weight(w, L, dgrad=True)), L.name
