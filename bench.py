@@ -99,6 +99,41 @@ def cpu_baseline(plan, seconds: float, batch: int):
                       f"(oracle/torch_port.py), {threads} threads, {cpu}"}
 
 
+def encoder_latents(model, plan, args, dev, world):
+    """BASELINE c4: encoder-only inference (encoder + mu head, the build_dictionary path) at
+    batch 1024 per GPU on synthetic patterns resident in HBM; no collective (every rank
+    encodes its own shard)."""
+    from latice import engine as E
+    from latice.seeding import synthetic_patterns
+    B = 1024
+    params = dict(model.named_parameters())
+    x = torch.from_numpy(synthetic_patterns(7, B, args.image_size)).to(dev)
+    packs = E.PackSet(plan, params).refresh()
+    with torch.no_grad():
+        for _ in range(2):
+            E.encode_latents(plan, x, params, packs)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.c4_batches):
+            mu = E.encode_latents(plan, x, params, packs)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    n = world * B * args.c4_batches
+    enc_flops = sum(2.0 * L.H * L.H * L.cin * L.cout * 9 for L in plan.enc) + 2 * plan.feat * plan.latent_dim
+    return {"metric": "encoder latents/sec (c4: encoder + mu head, batch 1024/GPU)",
+            "value": round(n / el, 1), "unit": "latents/s", "latents": n,
+            "ms_per_batch": round(el / args.c4_batches * 1e3, 3),
+            "tflops": round(enc_flops * n / el / 1e12, 2), "finite": bool(torch.isfinite(mu).all())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,14 +146,24 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
+    ap.add_argument("--c4-batches", type=int, default=64,
+                    help="encoder-only inference batches of 1024 for the c4 latents/s field (0: skip)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
+                         "several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; modulo only matters when rehearsing several ranks on one GPU
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = torch.device(f"cuda:{local}")
 
     from latice import engine as E
@@ -198,6 +243,8 @@ def main():
         "loss": round(loss, 6),
         "kernel_families_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in fam.items()},
     }
+    if args.c4_batches > 0:
+        res["c4_encoder_latents"] = encoder_latents(model, plan, args, dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline ...")
         res["cpu_baseline"] = cpu_baseline(plan, args.cpu_seconds, args.cpu_batch)

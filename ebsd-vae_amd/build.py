@@ -5,6 +5,8 @@ the repo snapshot to the GPU box.  Incremental: an object is rebuilt only when i
 common.h or the public header is newer.
 
     python ebsd-vae_amd/build.py [-j N] [--force]
+    python ebsd-vae_amd/build.py --variant NAME -D FLAG ...   # experiment build (A/B timing):
+        lib/libebsdvae_NAME.so with -DFLAG..., selected at run time by EBSDVAE_LIB=<path>
 """
 from __future__ import annotations
 
@@ -44,41 +46,47 @@ def _stale(src: str, obj: str) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src: str, force: bool) -> str:
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def _compile(src: str, force: bool, objdir: str = OBJ, defines=()) -> str:
+    obj = os.path.join(objdir, os.path.basename(src) + ".o")
     if force or _stale(src, obj):
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-               "-Wall", "-Wno-unused-function", "-c", src, "-o", obj]
+               "-Wall", "-Wno-unused-function"] + [f"-D{d}" for d in defines] + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(jobs: int = 8, force: bool = False, verbose: bool = True, variant: str = "",
+          defines=()) -> str:
+    objdir = OBJ if not variant else os.path.join(OBJ, variant)
+    lib = LIB if not variant else os.path.join(LIB_DIR, f"libebsdvae_{variant}.so")
+    os.makedirs(objdir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        tmp = LIB + ".tmp"
+        objs = list(ex.map(lambda s: _compile(s, force or bool(variant), objdir, defines), srcs))
+    LIB_ = lib
+    if force or not os.path.exists(LIB_) or any(os.path.getmtime(o) > os.path.getmtime(LIB_) for o in objs):
+        tmp = LIB_ + ".tmp"
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, LIB)
+        os.replace(tmp, LIB_)
     if verbose:
-        print(f"built {LIB}")
-    return LIB
+        print(f"built {LIB_}")
+    return LIB_
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
     a = ap.parse_args()
-    build(a.j, a.force)
+    build(a.j, a.force, variant=a.variant, defines=a.defines)
 
 
 if __name__ == "__main__":

@@ -101,7 +101,9 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         const float v = acc[mf][nf][r] + bb;
         acc[mf][nf][r] = v;
         s += v;
+#ifndef EV_TIMING_PROBE_NOEPI   // timing experiment only: no output traffic (wrong results)
         if (bvalid) y[(((size_t)gb * H + h0) * W + rem) * Cout + co] = v;
+#endif
       }
     if (FP != FP_NONE && bvalid) {
       // loads in batches of 32 issued before any use (latency overlapped within a batch)
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_big_kernel(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int HP = TH + 2, WP = W + 2;
   const int pixP = HP * WP;
-  const int xslab = pixP * CKP;
+  const int xslab = (pixP + 1) * CKP;   // + one dummy pixel slot for out-of-halo items
   float* lw0 = smem;
   float* lx0 = smem + 2 * WSLAB;
 
@@ -237,25 +239,31 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_big_kernel(
   float4 raw[KX][NR];
   float2 st[4];
   int cur_ch = 0;   // chunk whose halo is held in raw[]
+  // Branch-free staging: padding items load from a safe in-range address and are zeroed by
+  // select; items past the halo write a dummy LDS pixel slot (pixP).  Per-item divergent
+  // branches cost ~25 SALU + exec juggling per item inside the MFMA loop.
   auto issue_halo = [&](int ch) {
     cur_ch = ch;
     const int c = ch * CK + q * 4;
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
-      if (hw[k] >= 0) {
-        const int gh = hw[k] >> 16, gw = hw[k] & 0xffff;
-        if (POOL) {
-          const float* p = sb + ((size_t)(2 * gh) * Ws + 2 * gw) * Cin + c;
-          const size_t rs = (size_t)Ws * Cin;
-          raw[k][0] = ld4(p);
-          raw[k][NR > 1 ? 1 : 0] = ld4(p + Cin);
-          raw[k][NR > 2 ? 2 : 0] = ld4(p + rs);
-          raw[k][NR > 3 ? 3 : 0] = ld4(p + rs + Cin);
-        } else if (UPS) {
-          raw[k][0] = ld4(sb + ((size_t)(gh >> 1) * Ws + (gw >> 1)) * Cin + c);
-        } else {
-          raw[k][0] = ld4(sb + ((size_t)gh * Ws + gw) * Cin + c);
-        }
+      const int hv = hw[k] < 0 ? 0 : hw[k];
+      const int gh = hv >> 16, gw = hv & 0xffff;
+#ifdef EV_TIMING_PROBE_NOHALO   // timing experiment only: no halo traffic (wrong results)
+      raw[k][0] = make_float4(gh, gw, 1.f, 1.f);
+      continue;
+#endif
+      if (POOL) {
+        const float* p = sb + ((size_t)(2 * gh) * Ws + 2 * gw) * Cin + c;
+        const size_t rs = (size_t)Ws * Cin;
+        raw[k][0] = ld4(p);
+        raw[k][NR > 1 ? 1 : 0] = ld4(p + Cin);
+        raw[k][NR > 2 ? 2 : 0] = ld4(p + rs);
+        raw[k][NR > 3 ? 3 : 0] = ld4(p + rs + Cin);
+      } else if (UPS) {
+        raw[k][0] = ld4(sb + ((size_t)(gh >> 1) * Ws + (gw >> 1)) * Cin + c);
+      } else {
+        raw[k][0] = ld4(sb + ((size_t)gh * Ws + gw) * Cin + c);
       }
     }
     if (NORM) {
@@ -272,24 +280,23 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_big_kernel(
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
       const int pix = (tid + NTHR * k) >> 1;
-      if (pix < pixP) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (hw[k] >= 0) {
-          v = raw[k][0];
-          if (POOL)
-            v = max4(max4(raw[k][0], raw[k][NR > 1 ? 1 : 0]),
-                     max4(raw[k][NR > 2 ? 2 : 0], raw[k][NR > 3 ? 3 : 0]));
-          if (NORM)
-            v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]),
-                            normact_fs(v.z, fs[2]), normact_fs(v.w, fs[3]));
-          // interior pixels: optionally materialise the (pooled) activation for the wgrad
-          const int gh = hw[k] >> 16, gw = hw[k] & 0xffff;
-          if (act_out && gh >= h0 && gh < h0 + TH)
-            st4(act_out + (((size_t)b0 * H + gh) * W + gw) * Cin + cur_ch * CK + q * 4, v);
-        }
-        float* d = lx + pix * CKP + q * 4;
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+      float4 v = raw[k][0];
+      if (POOL)
+        v = max4(max4(raw[k][0], raw[k][NR > 1 ? 1 : 0]),
+                 max4(raw[k][NR > 2 ? 2 : 0], raw[k][NR > 3 ? 3 : 0]));
+      if (NORM)
+        v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]), normact_fs(v.z, fs[2]),
+                        normact_fs(v.w, fs[3]));
+      const bool ok = hw[k] >= 0;
+      v = make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+      // interior pixels: optionally materialise the (pooled) activation for the wgrad
+      if (act_out) {   // uniform (kernel argument)
+        const int gh = hw[k] >> 16, gw = hw[k] & 0xffff;
+        if (ok && gh >= h0 && gh < h0 + TH)
+          st4(act_out + (((size_t)b0 * H + gh) * W + gw) * Cin + cur_ch * CK + q * 4, v);
       }
+      float* d = lx + (pix < pixP ? pix : pixP) * CKP + q * 4;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
   };
   auto issue_weights = [&](int ch, float* lw) {
@@ -525,7 +532,7 @@ static bool plan_conv(int H, int W, int cin, int cout, Cfg* c) {
     c->KX = (pix * 2 + nthr - 1) / nthr;
     const int kxmax = cout == 128 ? 2 : (cout == 64 ? 5 : 9);
     if (c->KX > kxmax) return false;
-    c->lds = (2 * (size_t)9 * CK * cout + 2 * (size_t)pix * CKP) * sizeof(float);
+    c->lds = (2 * (size_t)9 * CK * cout + 2 * (size_t)(pix + 1) * CKP) * sizeof(float);
     return c->lds <= 160 * 1024;
   }
   // small images (8x8): one 64-pixel band per block, 64-wide Cout column blocks

@@ -21,6 +21,9 @@ constexpr int HT = 1024;         // threads per pattern
 constexpr int HW_ = HT / 64;     // waves per pattern
 constexpr int OCH = 32;          // head outputs per register chunk
 
+// MU_ONLY: the encoder-only inference path (DiffractionPatternIndexer.build_dictionary
+// consumes mu alone, latice/index/dp_indexer.py:136): only the mu head is evaluated.
+template <bool MU_ONLY>
 __global__ __launch_bounds__(HT) void heads_fwd_kernel(
     const float* __restrict__ enc, const float* __restrict__ wmu, const float* __restrict__ bmu,
     const float* __restrict__ wlv, const float* __restrict__ blv, const float* __restrict__ w2,
@@ -39,8 +42,10 @@ __global__ __launch_bounds__(HT) void heads_fwd_kernel(
     f[c * S * S + hw] = e[i];
   }
   __syncthreads();
-  for (int k = tid; k < F; k += HT) flat[(size_t)b * F + k] = f[k];
-  for (int o0 = 0; o0 < 2 * L; o0 += OCH) {
+  if (!MU_ONLY)
+    for (int k = tid; k < F; k += HT) flat[(size_t)b * F + k] = f[k];
+  const int NO = MU_ONLY ? L : 2 * L;
+  for (int o0 = 0; o0 < NO; o0 += OCH) {
     float acc[OCH];
 #pragma unroll
     for (int j = 0; j < OCH; ++j) acc[j] = 0.f;
@@ -49,16 +54,24 @@ __global__ __launch_bounds__(HT) void heads_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < OCH; ++j) {
         const int o = o0 + j;
-        if (o < 2 * L) acc[j] = fmaf(fk, (o < L) ? wmu[(size_t)o * F + k] : wlv[(size_t)(o - L) * F + k], acc[j]);
+        if (o < NO) acc[j] = fmaf(fk, (o < L) ? wmu[(size_t)o * F + k] : wlv[(size_t)(o - L) * F + k], acc[j]);
       }
     }
 #pragma unroll
     for (int j = 0; j < OCH; ++j) {
       const float v = wave_sum(acc[j]);
-      if (lane == 0 && o0 + j < 2 * L) red[wave * 2 * MAXL + o0 + j] = v;
+      if (lane == 0 && o0 + j < NO) red[wave * 2 * MAXL + o0 + j] = v;
     }
   }
   __syncthreads();
+  if (MU_ONLY) {
+    if (tid < L) {
+      float m = bmu[tid];
+      for (int w = 0; w < HW_; ++w) m += red[w * 2 * MAXL + tid];
+      mu[(size_t)b * L + tid] = m;
+    }
+    return;
+  }
   if (tid < L) {
     float m = bmu[tid], lv = blv[tid];
     for (int w = 0; w < HW_; ++w) {
@@ -331,12 +344,30 @@ extern "C" int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const floa
   EV_REQUIRE(lds <= 160 * 1024, "heads_fwd: feature width %d too large", F);
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)heads_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)heads_fwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
-  hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(HT), lds, (hipStream_t)stream, enc, w_mu, b_mu,
+  hipLaunchKernelGGL(heads_fwd_kernel<false>, dim3(B), dim3(HT), lds, (hipStream_t)stream, enc, w_mu, b_mu,
                      w_lv, b_lv, w_l2, b_l2, eps, flat, mu, std, z, dec_in, C, S, L);
   return evh::check_launch("heads_fwd");
+}
+
+extern "C" int ebsdvae_latent_mu(const float* enc, const float* w_mu, const float* b_mu, float* mu,
+                                 int B, int C, int S, int L, ebsdvae_stream_t stream) {
+  EV_REQUIRE(enc && w_mu && b_mu && mu, "latent_mu: null pointer");
+  EV_REQUIRE(B > 0 && L > 0 && L <= MAXL && C > 0 && S > 0, "latent_mu: bad shape L=%d", L);
+  const int F = C * S * S;
+  const size_t lds = (F + (HW_ * 2 + 1) * MAXL) * sizeof(float);
+  EV_REQUIRE(lds <= 160 * 1024, "latent_mu: feature width %d too large", F);
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)heads_fwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(heads_fwd_kernel<true>, dim3(B), dim3(HT), lds, (hipStream_t)stream, enc, w_mu,
+                     b_mu, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, mu, nullptr, nullptr,
+                     nullptr, C, S, L);
+  return evh::check_launch("latent_mu");
 }
 
 extern "C" int ebsdvae_heads_bwd(const float* g_dec, const float* g_z, const float* g_mu,

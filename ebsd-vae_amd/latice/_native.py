@@ -48,6 +48,7 @@ SIGNATURES = {
     "ebsdvae_in_bwd_first_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_latent_mu": [P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_wgrad_work": [I, I, I],
     "ebsdvae_heads_wgrad": [P, P, P, P, P, P, P, P, P, P, I, I, I, P],
     "ebsdvae_linear_fwd": [P, P, P, P, I, I, I, P],

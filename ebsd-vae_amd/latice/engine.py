@@ -346,21 +346,23 @@ def _wp(packs, name, k):
     return None if packs is None else packs[name][k]
 
 
-def encoder_forward(plan: Plan, x, params, packs=None):
+def encoder_forward(plan: Plan, x, params, packs=None, train=True):
     """x: (B,1,S,S) fp32 (== NHWC).  Returns (enc_out NHWC (B,s,s,C), saved).
-    packs: PackSet.refresh() result (None: pack each weight on the fly)."""
+    packs: PackSet.refresh() result (None: pack each weight on the fly).
+    train=False (inference): skip the pooled activations only the weight gradient needs."""
     B = x.shape[0]
     saved = {}
     src, sst = x, None
     for L in plan.enc:
         w, b = params[L.name + ".weight"], params[L.name + ".bias"]
         wp = _wp(packs, L.name, 0)
-        if L.src_mode == ACT_NORM_POOL:
+        if train and L.src_mode == ACT_NORM_POOL:
             y, st, act = conv_forward(src, sst, L, w, b, B, keep_act=True, wp=wp)
             saved[L.name + ".act_in"] = act
         else:
             y, st = conv_forward(src, sst, L, w, b, B, wp=wp)
-        saved[L.name] = (y, st)
+        if train:
+            saved[L.name] = (y, st)
         src, sst = y, st
     s, C = plan.enc_side, plan.enc_channels
     out = _empty(B, s, s, C, like=x)
@@ -408,6 +410,16 @@ def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=Fa
             N.call("ebsdvae_conv3x3_cout1_fwd", N.ptr(gy), None, ACT_RAW, N.ptr(params[wn]), None,
                    N.ptr(gx), 1, B, H, W, L.cout, N.stream())
     return out, gx
+
+
+def encode_latents(plan: Plan, x, params, packs=None):
+    """Encoder-only inference (BASELINE c4, build_dictionary): x (B,1,S,S) -> mu (B,L)."""
+    enc, _ = encoder_forward(plan, x, params, packs=packs, train=False)
+    B = x.shape[0]
+    mu = _empty(B, plan.latent_dim, like=x)
+    N.call("ebsdvae_latent_mu", N.ptr(enc), N.ptr(params["mu.0.weight"]), N.ptr(params["mu.0.bias"]),
+           N.ptr(mu), B, plan.enc_channels, plan.enc_side, plan.latent_dim, N.stream())
+    return mu
 
 
 # ----------------------------------------------------------------------------- heads

@@ -99,6 +99,16 @@ class VariationalAutoEncoder(nn.Module):
         x_hat = self.decoder(dec_in)
         return z, x_hat, mu, std
 
+    @torch.no_grad()
+    def encode_mu(self, x: torch.Tensor) -> torch.Tensor:
+        """Encoder-only fast path: mu == forward(x)[2] (the only output
+        DiffractionPatternIndexer.build_dictionary keeps, latice/index/dp_indexer.py:136),
+        without the reparameterisation and decoder."""
+        if x.device.type != "cuda":
+            raise RuntimeError("encode_mu needs a ROCm device tensor (no CPU fallback)")
+        params = dict(self.named_parameters())
+        return E.encode_latents(self._plan, x.contiguous(), params)
+
     @staticmethod
     def weights_init(m: nn.Module) -> None:
         """Kept for API parity with latice/model.py:68-80."""

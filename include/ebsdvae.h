@@ -169,6 +169,10 @@ int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const float* b_mu,
                       const float* b_l2, const float* eps, float* flat, float* mu,
                       float* std, float* z, float* dec_in, int B, int C, int S, int L,
                       ebsdvae_stream_t stream);
+/* Encoder-only inference head: mu = Linear(F,L)(flatten_NCHW(enc)) (latice/model.py:55-58;
+ * DiffractionPatternIndexer.build_dictionary consumes mu alone). */
+int ebsdvae_latent_mu(const float* enc, const float* w_mu, const float* b_mu, float* mu, int B,
+                      int C, int S, int L, ebsdvae_stream_t stream);
 /* g_dec: grad of dec_in (B,S,S,C NHWC); g_z/g_mu/g_std: direct output grads (may be
  * NULL = 0).  Writes g_enc (B,S,S,C NHWC) and per-sample scratch
  * gs = [g_mu_tot (B,L) | g_logvar (B,L) | g_out (B,F)] consumed by heads_wgrad. */

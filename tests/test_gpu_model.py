@@ -137,3 +137,14 @@ def test_batch_independence_at_full_size(cuda):
     outs, _ = O.forward({k: v.numpy() for k, v in sd.items()}, x[:2].cpu().numpy(), eps[:2].cpu().numpy())
     assert O.rel_err(h(mu[:2]), outs["mu"]) < 1e-4
     assert O.rel_err(h(xh[:2]), outs["x_hat"]) < 1e-4
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_encoder_only_latents_vs_reference(cuda, name):
+    """encode_mu (the build_dictionary fast path, BASELINE c4) == the reference's mu."""
+    f = O.load_fixture(os.path.join(GOLDEN, name + ".npz"))
+    m = build(f, cuda)
+    mu = m.encode_mu(torch.from_numpy(f["x"]).to(cuda))
+    assert O.rel_err(h(mu), f["mu"]) < 1e-4
+    _, _, mu_full, _ = m(torch.from_numpy(f["x"]).to(cuda), eps=torch.from_numpy(f["eps"]).to(cuda))
+    assert torch.allclose(mu, mu_full.detach(), rtol=0, atol=1e-6)
