@@ -2,7 +2,7 @@
 
 Plain hipcc, in-tree output (ebsd-vae_amd/lib/libebsdvae.so) so the library travels with
 the repo snapshot to the GPU box.  Incremental: an object is rebuilt only when its source,
-common.h or the public header is newer.
+a csrc header or the public header is newer.
 
     python ebsd-vae_amd/build.py [-j N] [--force]
     python ebsd-vae_amd/build.py --variant NAME -D FLAG ...   # experiment build (A/B timing):
@@ -42,7 +42,7 @@ def _stale(src: str, obj: str) -> bool:
     if not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
-    deps = [src, os.path.join(CSRC, "common.h"), HEADER]
+    deps = [src, HEADER] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

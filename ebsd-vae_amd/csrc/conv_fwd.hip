@@ -27,131 +27,12 @@
 // whole images per block, Cout split over blockIdx.y to fill the 256 CUs.
 // Epilogue (both): + bias, coalesced 128-B row stores of y, and per-wave InstanceNorm
 // partials {mean, M2} (Chan-combinable, no E[x^2]-E[x]^2 cancellation).
-#include "common.h"
-#include "../../include/ebsdvae.h"
+#include "conv_common.h"
 
 namespace ev {
 
 constexpr int CK = 8;        // input channels per K chunk
 constexpr int CKP = CK + 1;  // LDS pixel stride of the input halo
-
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-EV_DEVINL void glds16(const float* g, float* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const void*)g, (lds_void_ptr)lds_wave_base, 16, 0, 0);
-}
-
-// ------------------------------------------------------------------ shared epilogue
-constexpr int FP_NONE = -1;   // no fused InstanceNorm-backward reduce
-
-// Fused InstanceNorm-backward reduce of the PREVIOUS block (input-gradient convs only):
-// this conv's output is g = d loss / d a_prev (a_prev = [pool|up](lrelu(IN(y_prev))) at
-// this conv's resolution).  Per element it adds g_a = g * lrelu'(xhat) and g_a * xhat of
-// the y_prev pixel that g routes to (identity, the 2x2 argmax, or the upsample parent)
-// -- the sums ebsdvae_in_bwd_reduce would compute, without re-reading g.
-// y_prev offset (in pixels of y_prev) of the k-th value read for conv pixel pl
-template <int FP>
-EV_DEVINL int inbwd_pix(int pl, int W, int lW, int k) {
-  const int h = pl >> lW, w = pl & (W - 1);
-  if (FP == P_ID) return pl;
-  if (FP == P_UP) return (h >> 1) * (W >> 1) + (w >> 1);
-  return (2 * h + (k >> 1)) * (2 * W) + 2 * w + (k & 1);   // P_POOL window (k = dy*2+dx)
-}
-
-template <int FP>
-EV_DEVINL void inbwd_acc(float g, const float* v, float2 sp, float& s1, float& s2) {
-  float x = (v[0] - sp.x) * sp.y;
-  if (FP == P_POOL) {   // first maximum of lrelu(xhat) in window order (0,0),(0,1),(1,0),(1,1)
-    float best = lrelu(x);
-#pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      const float xk = (v[k] - sp.x) * sp.y;
-      const float f = lrelu(xk);
-      if (f > best) { best = f; x = xk; }
-    }
-  }
-  const float ga = g * slope(x);
-  s1 += ga;
-  s2 = fmaf(ga, x, s2);
-}
-
-template <int MF, int NF, int FP>
-EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bias,
-                             float* __restrict__ y, float2* __restrict__ spart, int B, int H,
-                             int W, int Cout, int b0, int h0, int tpx, int wpx0, int co_base,
-                             int hk, int l32, const float* __restrict__ yprev,
-                             const float2* __restrict__ stprev, double2* __restrict__ ipart) {
-  constexpr int MW = MF * 32;
-  const int wimg = wpx0 / tpx;  // the wave's pixels lie in ONE image
-  const int gb = b0 + wimg;
-  const bool bvalid = gb < B;
-  const int T = (H * W) / MW;
-  const int slot = (h0 * W + (wpx0 - wimg * tpx)) / MW;
-#pragma unroll
-  for (int nf = 0; nf < NF; ++nf) {
-    const int co = co_base + nf * 32 + l32;
-    const float bb = bias ? bias[co] : 0.f;
-    float s = 0.f;
-#pragma unroll
-    for (int mf = 0; mf < MF; ++mf)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = wpx0 + mf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-        const int rem = m - wimg * tpx;
-        const float v = acc[mf][nf][r] + bb;
-        acc[mf][nf][r] = v;
-        s += v;
-#ifndef EV_TIMING_PROBE_NOEPI   // timing experiment only: no output traffic (wrong results)
-        if (bvalid) y[(((size_t)gb * H + h0) * W + rem) * Cout + co] = v;
-#endif
-      }
-    if (FP != FP_NONE && bvalid) {
-      // loads in batches of 32 issued before any use (latency overlapped within a batch)
-      constexpr int NL = FP == P_POOL ? 4 : 1;
-      constexpr int G = (32 / NL) < MF * 16 ? (32 / NL) : MF * 16;
-      static_assert((MF * 16) % G == 0, "batch size");
-      const int lW = 31 - __builtin_clz(W);
-      const size_t plane = FP == P_POOL ? (size_t)4 * H * W : (FP == P_UP ? (size_t)(H * W) / 4 : (size_t)H * W);
-      const float* yp = yprev + (size_t)gb * plane * Cout + co;
-      const float2 sp = stprev[(size_t)gb * Cout + co];
-      const int pbase = h0 * W - wimg * tpx + wpx0 + 4 * hk;
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int e0 = 0; e0 < MF * 16; e0 += G) {
-        float v[G][NL];
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const int e = e0 + j, mf = e >> 4, r = e & 15;
-          const int pl = pbase + mf * 32 + (r & 3) + 8 * (r >> 2);
-#pragma unroll
-          for (int k = 0; k < NL; ++k) v[j][k] = yp[(size_t)inbwd_pix<FP>(pl, W, lW, k) * Cout];
-        }
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const int e = e0 + j;
-          inbwd_acc<FP>(acc[e >> 4][nf][e & 15], v[j], sp, s1, s2);
-        }
-      }
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (hk == 0) ipart[((size_t)gb * T + slot) * Cout + co] = make_double2((double)s1, (double)s2);
-    }
-    if (spart) {
-      s += __shfl_xor(s, 32, 64);
-      const float mean = s * (1.0f / MW);
-      float q = 0.f;
-#pragma unroll
-      for (int mf = 0; mf < MF; ++mf)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float d = acc[mf][nf][r] - mean;
-          q = fmaf(d, d, q);
-        }
-      q += __shfl_xor(q, 32, 64);
-      if (hk == 0 && bvalid) spart[((size_t)gb * T + slot) * Cout + co] = make_float2(mean, q);
-    }
-  }
-}
 
 // 9 taps x 4 k-pairs of one 8-channel chunk: A from the halo, B from the weight slab
 template <int MF, int NF>
@@ -469,10 +350,6 @@ __global__ void pack_conv_weight_kernel(const float* __restrict__ s, float* __re
   }
 }
 
-struct PackBatch {
-  ebsdvae_pack_desc d[EBSDVAE_MAX_PACK];
-};
-
 // one launch packs every conv weight of a step: blockIdx.y = descriptor (kernel argument)
 __global__ void pack_conv_weights_kernel(const PackBatch pb) {
   const ebsdvae_pack_desc& q = pb.d[blockIdx.y];
@@ -551,13 +428,6 @@ template <typename K>
 static void allow_big_lds(K k) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
-
-// fused InstanceNorm-backward reduce arguments of input-gradient launches (FP != FP_NONE)
-struct InBwdFuse {
-  const float* yprev = nullptr;
-  const float2* stprev = nullptr;
-  double2* part = nullptr;
-};
 
 template <int NWV, int WM, int MF, int NF, int KX, int MODE, int FP>
 static void launch_big1(const Cfg& c, const float* src, const float* st, const float* wp,

@@ -30,6 +30,12 @@ SIGNATURES = {
     "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_stat_tiles": [I, I, I],
     "ebsdvae_conv3x3_dgrad_inbwd": [P, P, P, P, P, I, P, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_split_supported": [I, I, I, I, I],
+    "ebsdvae_conv3x3_split_stat_tiles": [I, I, I],
+    "ebsdvae_pack_split_bytes": [I, I, I],
+    "ebsdvae_pack_conv_weights_split": [P, I, I, P],
+    "ebsdvae_conv3x3_fwd_split": [P, P, I, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_dgrad_inbwd_split": [P, P, P, P, P, I, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_fwd": [P, P, I, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],
     "ebsdvae_conv3x3_wgrad_slices": [I, I, I, I, I],
@@ -61,10 +67,12 @@ SIGNATURES = {
     "ebsdvae_adam": [P, P, P, P, P, P, I64, F, F, F, F, F, I, P],
 }
 _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t,
-            "ebsdvae_heads_wgrad_work": ctypes.c_size_t}
+            "ebsdvae_heads_wgrad_work": ctypes.c_size_t, "ebsdvae_pack_split_bytes": ctypes.c_size_t}
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
-           "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work"}
+           "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
+           "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
+           "ebsdvae_pack_split_bytes"}
 
 _lib = None
 _lock = threading.Lock()

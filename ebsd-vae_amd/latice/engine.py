@@ -19,6 +19,7 @@ from the PyTorch caching allocator and every launch goes to the current HIP stre
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -159,42 +160,105 @@ def _empty(*shape, like):
     return torch.empty(shape, dtype=torch.float32, device=like.device)
 
 
-def pack_weight(w, layer: ConvLayer, dgrad: bool):
+# ----------------------------------------------------------------------------- precision
+# Conv arithmetic (csrc/conv_fwd.hip, csrc/conv_split.hip):
+#   "fp32"   v_mfma_f32_32x32x2_f32 (exact fp32 products);
+#   "bf16x6" 3-piece split-bf16 MFMA, 6 products per fp32 product (~2^-25, fp32 grade);
+#   "bf16x3" 2-piece split-bf16 MFMA, 3 products (~2^-16.5 per product).
+# Split modes cover every conv layer the split kernel supports (Cout in {32,64,128},
+# H*W >= 256); the others stay fp32.
+_PIECES = {"fp32": 0, "bf16x3": 2, "bf16x6": 3}
+_PRECISION = os.environ.get("EBSDVAE_PRECISION", "fp32")
+if _PRECISION not in _PIECES:
+    raise ValueError(f"EBSDVAE_PRECISION must be one of {sorted(_PIECES)}")
+_SPLIT_CACHE = {}
+
+
+def set_precision(mode: str):
+    global _PRECISION
+    if mode not in _PIECES:
+        raise ValueError(f"precision must be one of {sorted(_PIECES)}, not {mode!r}")
+    _PRECISION = mode
+
+
+def get_precision() -> str:
+    return _PRECISION
+
+
+def split_pieces(H: int, cin: int, cout: int) -> int:
+    """bf16 pieces per operand of a conv with input channels cin -> cout at HxH (0 = fp32)."""
+    np_ = _PIECES[_PRECISION]
+    if np_ == 0:
+        return 0
+    key = (H, cin, cout, np_)
+    if key not in _SPLIT_CACHE:
+        ok = N.call("ebsdvae_conv3x3_split_supported", H, H, cin, cout, np_)
+        _SPLIT_CACHE[key] = np_ if ok else 0
+    return _SPLIT_CACHE[key]
+
+
+@dataclass
+class PackedW:
+    t: torch.Tensor
+    pieces: int   # 0 = fp32 pack
+
+
+def _pack_numel(layer: ConvLayer, pieces: int, dgrad: bool) -> int:
+    if not pieces:
+        return 9 * layer.cin * layer.cout
     ci_, co_ = (layer.cout, layer.cin) if dgrad else (layer.cin, layer.cout)
-    out = _empty(9 * ci_ * co_, like=w)
-    N.call("ebsdvae_pack_conv_weight", N.ptr(w), N.ptr(out), layer.cin, layer.cout,
-           layer.kind, int(dgrad), N.stream())
-    return out
+    return N.call("ebsdvae_pack_split_bytes", ci_, co_, pieces) // 4
+
+
+def pack_weight(w, layer: ConvLayer, dgrad: bool) -> PackedW:
+    ci_, co_ = (layer.cout, layer.cin) if dgrad else (layer.cin, layer.cout)
+    np_ = split_pieces(layer.H, ci_, co_)
+    out = _empty(_pack_numel(layer, np_, dgrad), like=w)
+    if np_:
+        d = (N.PackDesc * 1)(N.PackDesc(N.ptr(w), N.ptr(out), layer.cin, layer.cout, layer.kind, int(dgrad)))
+        N.call("ebsdvae_pack_conv_weights_split", ctypes.addressof(d), 1, np_, N.stream())
+    else:
+        N.call("ebsdvae_pack_conv_weight", N.ptr(w), N.ptr(out), layer.cin, layer.cout,
+               layer.kind, int(dgrad), N.stream())
+    return PackedW(out, np_)
 
 
 class PackSet:
     """Packed forward / input-gradient weights of every conv layer of a plan, refreshed by
-    ONE batched launch (ebsdvae_pack_conv_weights) per step.  The parameter tensors must
-    keep their storage (e.g. views into the trainer's flat buffer)."""
+    one batched launch per precision (ebsdvae_pack_conv_weights[_split]) per step.  The
+    parameter tensors must keep their storage (e.g. views into the trainer's flat buffer)."""
 
     def __init__(self, plan: "Plan", params):
         self.packs = {}
-        descs = []
+        descs = {}
         for i, L in enumerate(plan.enc):
             self._add(L, params[L.name + ".weight"], dgrad=i > 0, descs=descs)
         for L in plan.dec:
             self._add(L, params[L.name + ".weight"], dgrad=True, descs=descs)
-        if len(descs) > N.MAX_PACK:
-            raise RuntimeError(f"PackSet: {len(descs)} packs > {N.MAX_PACK}")
-        self.n = len(descs)
-        self.descs = (N.PackDesc * self.n)(*descs)
+        self.batches = []
+        for np_, lst in sorted(descs.items()):
+            if len(lst) > N.MAX_PACK:
+                raise RuntimeError(f"PackSet: {len(lst)} packs > {N.MAX_PACK}")
+            self.batches.append((np_, (N.PackDesc * len(lst))(*lst), len(lst)))
+
+    def _one(self, L, w, dgrad, descs):
+        ci_, co_ = (L.cout, L.cin) if dgrad else (L.cin, L.cout)
+        np_ = split_pieces(L.H, ci_, co_)
+        t = _empty(_pack_numel(L, np_, dgrad), like=w)
+        descs.setdefault(np_, []).append(N.PackDesc(N.ptr(w), N.ptr(t), L.cin, L.cout, L.kind, int(dgrad)))
+        return PackedW(t, np_)
 
     def _add(self, L, w, dgrad, descs):
-        pf = _empty(9 * L.cin * L.cout, like=w)
-        descs.append(N.PackDesc(N.ptr(w), N.ptr(pf), L.cin, L.cout, L.kind, 0))
-        pd = None
-        if dgrad:
-            pd = _empty(9 * L.cin * L.cout, like=w)
-            descs.append(N.PackDesc(N.ptr(w), N.ptr(pd), L.cin, L.cout, L.kind, 1))
+        pf = self._one(L, w, False, descs)
+        pd = self._one(L, w, True, descs) if dgrad else None
         self.packs[L.name] = (pf, pd)
 
     def refresh(self):
-        N.call("ebsdvae_pack_conv_weights", ctypes.addressof(self.descs), self.n, N.stream())
+        for np_, arr, n in self.batches:
+            if np_:
+                N.call("ebsdvae_pack_conv_weights_split", ctypes.addressof(arr), n, np_, N.stream())
+            else:
+                N.call("ebsdvae_pack_conv_weights", ctypes.addressof(arr), n, N.stream())
         return self.packs
 
 
@@ -206,13 +270,19 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     if wp is None:
         wp = pack_weight(w, layer, dgrad=False)
     y = _empty(B, H, H, layer.cout, like=w)
-    T = N.call("ebsdvae_conv3x3_stat_tiles", H, H, layer.cout)
+    T = N.call("ebsdvae_conv3x3_split_stat_tiles" if wp.pieces else "ebsdvae_conv3x3_stat_tiles",
+               H, H, layer.cout)
     part = _empty(B, T, layer.cout, 2, like=w)
     act = _empty(B, H, H, layer.cin, like=w) if keep_act else None
-    _launch("conv3x3_fwd", conv_flops(B, H, H, layer.cin, layer.cout), N.call,
-            "ebsdvae_conv3x3_fwd", N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp), N.ptr(b),
-            N.ptr(y), N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout, N.stream(),
-            tag=f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m{layer.src_mode}")
+    tag = f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m{layer.src_mode}"
+    args = (N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y),
+            N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout)
+    flops = conv_flops(B, H, H, layer.cin, layer.cout)
+    if wp.pieces:
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split", *args, wp.pieces,
+                N.stream(), tag=tag)
+    else:
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", *args, N.stream(), tag=tag)
     st = _empty(B, layer.cout, 2, like=w)
     N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
            N.stream())
@@ -322,16 +392,27 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None):
     tag = f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}"
     flops = conv_flops(B, H, W, layer.cin, layer.cout)
     if prev is None:
-        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW,
-                N.ptr(wd), None, N.ptr(gin), None, None, B, H, W, layer.cout, layer.cin,
-                N.stream(), tag=tag)
+        if wd.pieces:
+            _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_split", N.ptr(gy),
+                    N.ptr(wd.t), N.ptr(gin), None, None, -1, None, B, H, W, layer.cout, layer.cin,
+                    wd.pieces, N.stream(), tag=tag)
+        else:
+            _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW,
+                    N.ptr(wd.t), None, N.ptr(gin), None, None, B, H, W, layer.cout, layer.cin,
+                    N.stream(), tag=tag)
         return gin
     y_prev, st_prev, pmode = prev
-    T = N.call("ebsdvae_conv3x3_stat_tiles", H, W, layer.cin)
+    T = N.call("ebsdvae_conv3x3_split_stat_tiles" if wd.pieces else "ebsdvae_conv3x3_stat_tiles",
+               H, W, layer.cin)
     part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
-    _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd", N.ptr(gy), N.ptr(wd),
-            N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev), pmode, part.data_ptr(), B, H, W,
-            layer.cout, layer.cin, N.stream(), tag=tag + " +inbwd")
+    args = (N.ptr(gy), N.ptr(wd.t), N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev), pmode,
+            part.data_ptr(), B, H, W, layer.cout, layer.cin)
+    if wd.pieces:
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_split", *args, wd.pieces,
+                N.stream(), tag=tag + " +inbwd")
+    else:
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd", *args, N.stream(),
+                tag=tag + " +inbwd")
     return gin, part
 
 

@@ -97,6 +97,30 @@ int ebsdvae_conv3x3_cout1_fwd(const float* src, const float* src_stats, int src_
 int ebsdvae_conv3x3_cout1_dgrad(const float* g, const float* w, float* gin, int B, int H,
                                 int W, int cin, ebsdvae_stream_t stream);
 
+/* ---- split-bf16 conv: same semantics as ebsdvae_conv3x3_fwd / _dgrad_inbwd ---------------
+ * Each fp32 operand is carried as `pieces` bf16 pieces (x0 = bf16(x), x1 = bf16(x - x0),
+ * x2 = bf16(x - x0 - x1)) and every product keeps the terms of total order < pieces, on
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
+ *   pieces = 2 ("bf16x3", 3 MFMAs, ~2^-16.5 relative error per product);
+ *   pieces = 3 ("bf16x6", 6 MFMAs, ~2^-25: fp32 grade).
+ * Weights use the split pack ([cin'/8][tap 0..9][piece][cout'][8] bf16,
+ * ebsdvae_pack_split_bytes bytes).  Shapes: ebsdvae_conv3x3_split_supported; InstanceNorm
+ * partials use ebsdvae_conv3x3_split_stat_tiles tiles per image.  pmode = -1 in
+ * ebsdvae_conv3x3_dgrad_inbwd_split is a plain input gradient (y_prev/st_prev/part unused). */
+int ebsdvae_conv3x3_split_supported(int H, int W, int cin, int cout, int pieces);
+int ebsdvae_conv3x3_split_stat_tiles(int H, int W, int cout);
+size_t ebsdvae_pack_split_bytes(int cin, int cout, int pieces);
+int ebsdvae_pack_conv_weights_split(const ebsdvae_pack_desc* descs, int n, int pieces,
+                                    ebsdvae_stream_t stream);
+int ebsdvae_conv3x3_fwd_split(const float* src, const float* src_stats, int src_mode,
+                              const void* wpack, const float* bias, float* y, float* stat_part,
+                              float* act_out, int B, int H, int W, int cin, int cout, int pieces,
+                              ebsdvae_stream_t stream);
+int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpack, float* gin,
+                                      const float* y_prev, const float* st_prev, int pmode,
+                                      double* part, int B, int H, int W, int cin, int cout,
+                                      int pieces, ebsdvae_stream_t stream);
+
 /* ---- weight gradients (deterministic two-level reduction) -----------------------------
  * Partial dW[co][ci][tap] and db[co] over pixel slices; then ebsdvae_wgrad_reduce sums
  * the slices in fixed order into the parameter-gradient layout of `kind` (0 conv,

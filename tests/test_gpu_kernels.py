@@ -393,6 +393,72 @@ def test_batched_weight_pack_matches_single_packs(cuda):
     for i, L in enumerate(plan.enc + plan.dec):
         w = params[L.name + ".weight"]
         pf, pd = packs[L.name]
-        assert torch.equal(pf, E.pack_weight(w, L, dgrad=False)), L.name
+        single = E.pack_weight(w, L, dgrad=False)
+        assert pf.pieces == single.pieces and torch.equal(pf.t, single.t), L.name
         if pd is not None:
-            assert torch.equal(pd, E.pack_weight(w, L, dgrad=True)), L.name
+            single = E.pack_weight(w, L, dgrad=True)
+            assert pd.pieces == single.pieces and torch.equal(pd.t, single.t), L.name
+
+
+SPLIT_TOL = {"bf16x3": 1e-4, "bf16x6": 2e-5}   # ~2^-16.5 / ~2^-25 per product
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("cin,cout,H,mode", [c for c in FWD_CASES if c[0] > 1 and c[2] >= 16])
+def test_conv3x3_fwd_split_bf16(cuda, cin, cout, H, mode, prec):
+    """Split-bf16 forward == float64 oracle (bf16x3 within 1e-4, bf16x6 at fp32 grade)."""
+    if not N.call("ebsdvae_conv3x3_split_supported", H, H, cin, cout, {"bf16x3": 2, "bf16x6": 3}[prec]):
+        pytest.skip("shape not covered by the split kernel")
+    rng = np.random.default_rng(31 + cin + cout + H + mode)
+    B = 2
+    s, mean, rstd, st = make_src(rng, B, H, cin, mode)
+    w = rng.standard_normal((cout, cin, 3, 3)) * 0.1
+    b = rng.standard_normal(cout) * 0.1
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
+    old = E.get_precision()
+    E.set_precision(prec)
+    try:
+        y, stt = E.conv_forward(dev(s), dev(st) if mode in (1, 2, 4) else None, layer, dev(w), dev(b), B)
+    finally:
+        E.set_precision(old)
+    a = act_oracle(s, mean, rstd, mode)
+    ref = O.conv3x3(a, w, b)
+    assert O.rel_err(host(y), ref) < SPLIT_TOL[prec]
+    _, rm, rr = O.instance_norm(ref)
+    assert O.rel_err(host(stt)[..., 0], rm[:, 0, 0, :]) < 1e-4
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("cin,cout,H,pmode", [c for c in FUSED_CASES if c[2] >= 16])
+def test_dgrad_fused_split_bf16(cuda, cin, cout, H, pmode, prec):
+    rng = np.random.default_rng(41 + cin + cout + H + pmode)
+    B = 2
+    Hy = {E.P_ID: H, E.P_POOL: 2 * H, E.P_UP: H // 2}[pmode]
+    y = rng.standard_normal((B, Hy, Hy, cin)) * 2 + 0.5
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    gy = rng.standard_normal((B, H, H, cout))
+    wsrc = rng.standard_normal((cout, cin, 3, 3)) * 0.1
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, E.ACT_RAW, 0)
+    old = E.get_precision()
+    E.set_precision(prec)
+    try:
+        y_d, st_d = dev(y), dev(st)
+        gin, part = E.conv_dgrad(dev(gy), layer, dev(wsrc), prev=(y_d, st_d, pmode))
+        g_prev = E.in_backward(gin, pmode, y_d, st_d, part=part)
+        gin2 = E.conv_dgrad(dev(gy), layer, dev(wsrc))
+    finally:
+        E.set_precision(old)
+    gn = O.conv3x3_dgrad(gy, wsrc)
+    assert O.rel_err(host(gin), gn) < SPLIT_TOL[prec]
+    assert O.rel_err(host(gin2), gn) < SPLIT_TOL[prec]
+    a = O.lrelu(xh)
+    if pmode == E.P_POOL:
+        _, arg = O.maxpool2(a)
+        ga = O.maxpool2_bwd(gn, arg)
+    elif pmode == E.P_UP:
+        ga = O.upsample2_bwd(gn)
+    else:
+        ga = gn
+    ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
+    assert O.rel_err(host(g_prev), ref) < 2e-4

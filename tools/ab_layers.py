@@ -29,7 +29,7 @@ def run(spec):
         parts = line.rsplit(None, 2)
         if len(parts) == 3:
             try:
-                rows[parts[0].strip()] = float(parts[1])
+                rows[parts[0].replace(" x3", "").strip()] = float(parts[1])
             except ValueError:
                 pass
         elif line.startswith("total"):
