@@ -146,6 +146,8 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
+    ap.add_argument("--precision", default=None, choices=["fp32", "bf16x6", "bf16x3"],
+                    help="conv arithmetic (default: the engine default, bf16x6)")
     ap.add_argument("--c4-batches", type=int, default=64,
                     help="encoder-only inference batches of 1024 for the c4 latents/s field (0: skip)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -168,6 +170,8 @@ def main():
 
     from latice import engine as E
     from latice.model import VariationalAutoEncoderRawData
+    if args.precision:
+        E.set_precision(args.precision)
     from latice.seeding import seeded_state_dict, synthetic_patterns
     from latice.trainer import VAETrainer
 
@@ -217,12 +221,17 @@ def main():
         flops_per_launch = d["flops"] / d["launches"]
         avg_s = d["ms"] / d["launches"] / 1e3
         ach = flops_per_launch / avg_s / 1e12
+        # peak of the family's arithmetic (fp32 MFMA 157.3, or the bf16 MFMA peak over the
+        # split's products per fp32 product), flop-weighted over its launches
+        peak = d["flops"] / d["peak_s"] / 1e12
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
-                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": pmc_traffic(dom),
+                "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": pmc_traffic(dom),
                 "launches_per_step": d["launches"] // args.steps,
+                "split_bf16_launches_per_step": d["split_launches"] // args.steps,
                 "avg_launch_us": round(avg_s * 1e6, 2),
-                "gflop_per_launch": round(flops_per_launch / 1e9, 3)}
+                "gflop_per_launch": round(flops_per_launch / 1e9, 3),
+                "flops": "algorithmic fp32-equivalent (2*B*H*W*Cin*Cout*9 per conv)"}
     step_tflops = step_flops_per_pattern(plan) * args.batch / (ms / 1e3) / 1e12
 
     res = {
@@ -231,6 +240,11 @@ def main():
         "value": round(value, 2), "unit": "patterns/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "conv_arithmetic": E.get_precision() + {
+            "fp32": " (v_mfma_f32_32x32x2_f32)",
+            "bf16x6": " (fp32 operands split into 3 bf16 pieces, 6 bf16 MFMA products per fp32"
+                      " product, fp32 accumulation: fp32-grade, same parity gates as fp32)",
+            "bf16x3": " (2 bf16 pieces, 3 products: ~2^-16.5 per product)"}[E.get_precision()],
         "config": {"workload": f"c{2 if world == 1 else 3}: VariationalAutoEncoderRawData "
                                f"{args.image_size}x{args.image_size}, latent {args.latent_dim}, "
                                f"batch {args.batch}/GPU, fwd+loss+bwd+Adam"

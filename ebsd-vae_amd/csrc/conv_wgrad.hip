@@ -29,15 +29,16 @@ struct WgGeom {
   int TH, TW, NI, ntx, nty, tiles, slices, tps, lTW, ltpx;
 };
 
-static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
+// pt = pixels per tile (128 for fp32, 64 for the split-bf16 kernels)
+static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g, int pt = WG_PT) {
   g->TW = W < 32 ? W : 32;
-  if (H * g->TW >= WG_PT) {
-    g->TH = WG_PT / g->TW;
+  if (H * g->TW >= pt) {
+    g->TH = pt / g->TW;
     g->NI = 1;
   } else {
     g->TH = H;
-    g->NI = WG_PT / (H * W);
-    if (g->NI * H * W != WG_PT) return false;
+    g->NI = pt / (H * W);
+    if (g->NI * H * W != pt) return false;
   }
   if (W % g->TW || H % g->TH) return false;
   if (g->NI * (g->TH + 2) * (g->TW + 2) > 224) return false;   // KH = 7 halo items / thread
@@ -282,6 +283,275 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(
   }
 }
 
+// ------------------------------------------------------------------ split-bf16 (NP pieces)
+// Same blocking, slices and register prefetch as wgrad_kernel, on v_mfma_f32_16x16x32_bf16
+// with every operand split into NP bf16 pieces (products of total order < NP, see
+// conv_split.hip).  K = pixels: both operands are staged pixel-major (NHWC, as loaded) in
+// per-piece LDS images and read k-major with the hardware transpose read
+// ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 and
+// receives one column of the 4 rows).  Element j of a lane group g's fragment is pixel
+//     32 s + (j < 4 ? 4g + j : 16 + 4g + j - 4)
+// of the tile, which with row strides of 160 / 96 B keeps every transposed read
+// conflict-free; the tap shift is a per-lane row offset into the activation halo, so any
+// shift stays 8-byte aligned.
+template <int TW, int PT>
+struct WgTileP {
+  static constexpr int TH = PT == 128 ? (TW == 32 ? 4 : 8) : (TW == 32 ? 2 : (TW == 16 ? 4 : 8));
+  static constexpr int NI = (PT == 128 && TW == 8) ? 2 : 1;
+  static constexpr int HP = TH + 2, WP = TW + 2;
+  static constexpr int HALO = NI * HP * WP;
+  static constexpr int IPX = TH * TW;
+  static_assert(NI * IPX == PT, "tile pixels");
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4* lds_s16x4_ptr;
+
+EV_DEVINL bf16x8w tr_frag(const char* r0, const char* r1) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(r0));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(r1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8w, v);
+}
+
+template <int NP>
+EV_DEVINL void store_pieces(char* base, size_t piece_stride, float4 v) {
+  const float e[4] = {v.x, v.y, v.z, v.w};
+  typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+  bf4 pc[NP];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float r = e[c];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const __bf16 h = (__bf16)r;
+      pc[i][c] = h;
+      r -= (float)h;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NP; ++i) *reinterpret_cast<bf4*>(base + i * piece_stride) = pc[i];
+}
+
+constexpr int WGS_ASB = 96;   // activation image row stride (32 ch x 2 B + 32 B)
+
+template <int NP, int NWCO, int KSPLIT, int MODE, int TW, int PT>
+__global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
+    const float* __restrict__ src, const float2* __restrict__ sstats,
+    const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
+    int H, int W, int Cin, int Cout, WgGeom g) {
+  using T = WgTileP<TW, PT>;
+  constexpr int CO_T = NWCO * 32;
+  constexpr int GSB = CO_T * 2 + 32;      // gy image row stride (bytes)
+  constexpr int QG = CO_T / 4;
+  constexpr int KG = PT * CO_T / 4 / 256; // gy float4 items per thread per tile
+  constexpr int KH = (T::HALO * 8 + 255) / 256;
+  constexpr int KSTEPS = PT / 32;
+  constexpr size_t GY_PIECE = (size_t)PT * GSB;
+  constexpr size_t ACT_PIECE = (size_t)T::HALO * WGS_ASB;
+  constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_UP);
+  constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
+  static_assert(NWCO * 2 * KSPLIT == 4, "4 waves per block");
+  static_assert(KG >= 1, "gy items");
+  static_assert(MODE != ACT_NORM_POOL, "pool-fed layers use the materialised activation");
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  char* gimg = wsm;                         // [NP][PT][GSB]
+  char* aimg = wsm + NP * GY_PIECE;         // [NP][HALO][96]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
+  const int slice = blockIdx.x, co0 = blockIdx.y * CO_T, ci0 = blockIdx.z * 32;
+  const int Hs = UPS ? H / 2 : H, Ws = UPS ? W / 2 : W;
+  const int qh = tid & 7;
+  const int qg = tid % QG;
+  const bool do_bias = blockIdx.z == 0;
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double bs[4] = {0.0, 0.0, 0.0, 0.0};
+
+  const int per_img = g.ntx * g.nty;
+  const int t_beg = slice * g.tps;
+  const int t_end = min(t_beg + g.tps, g.tiles);
+  float4 rg[KG], rh[KH];
+  float2 st[T::NI][4];
+  int cb0 = 0, cy0 = 0, cx0 = 0;
+  auto load_stats = [&](int b0) {
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i) {
+      const int gb = min(b0 + i, B - 1);
+      const float2* sp = sstats + (size_t)gb * Cin + ci0 + qh * 4;
+      st[i][0] = sp[0]; st[i][1] = sp[1]; st[i][2] = sp[2]; st[i][3] = sp[3];
+    }
+  };
+  auto issue = [&](int t) {
+    const int ib = t / per_img, rr = t - ib * per_img;
+    const int ty = rr / g.ntx;
+    const int b0 = ib * T::NI, y0 = ty * T::TH, x0 = (rr - ty * g.ntx) * TW;
+    cb0 = b0; cy0 = y0; cx0 = x0;
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const int px = (tid + 256 * k) / QG;
+      const int img = px / T::IPX, rem = px % T::IPX;
+      const int r = rem / TW, c = rem % TW;
+      const int gb = b0 + img;
+      if (T::NI == 1 || gb < B)
+        rg[k] = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + qg * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      const int pix = (tid + 256 * k) >> 3;
+      const int img = pix / (T::HP * T::WP), rem = pix % (T::HP * T::WP);
+      const int hh = rem / T::WP, ww = rem % T::WP;
+      const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
+      if (pix < T::HALO && gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
+        const int sh = UPS ? (gh >> 1) : gh, sw = UPS ? (gw >> 1) : gw;
+        rh[k] = ld4(src + (((size_t)gb * Hs + sh) * Ws + sw) * Cin + ci0 + qh * 4);
+      }
+    }
+    if (NORM && T::NI == 1) load_stats(b0);
+  };
+  auto store = [&]() {
+    if (NORM && T::NI > 1) load_stats(cb0);
+    float4 tb = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const int px = (tid + 256 * k) / QG;
+      float4 v = rg[k];
+      if (T::NI > 1 && cb0 + px / T::IPX >= B) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      tb.x += v.x; tb.y += v.y; tb.z += v.z; tb.w += v.w;
+      store_pieces<NP>(gimg + px * GSB + qg * 8, GY_PIECE, v);
+    }
+    bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      const int pix = (tid + 256 * k) >> 3;
+      if (pix < T::HALO) {
+        const int img = pix / (T::HP * T::WP), rem = pix % (T::HP * T::WP);
+        const int hh = rem / T::WP, ww = rem % T::WP;
+        const int gh = cy0 + hh - 1, gw = cx0 + ww - 1, gb = cb0 + img;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
+          v = rh[k];
+          if (NORM) {
+            const bool second = T::NI > 1 && img > 0;
+            v = make_float4(normact(v.x, second ? st[T::NI - 1][0] : st[0][0]),
+                            normact(v.y, second ? st[T::NI - 1][1] : st[0][1]),
+                            normact(v.z, second ? st[T::NI - 1][2] : st[0][2]),
+                            normact(v.w, second ? st[T::NI - 1][3] : st[0][3]));
+          }
+        }
+        store_pieces<NP>(aimg + pix * WGS_ASB + qh * 8, ACT_PIECE, v);
+      }
+    }
+  };
+
+  // per-lane transposed-read geometry: lane 4q+p of group gq addresses row q, columns 4p..
+  const int gq = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+  const int acol = (wco * 32 + 4 * p4) * 2;          // gy image column bytes (+ f*32)
+  const int bcol = (wci * 16 + 4 * p4) * 2;          // act image column bytes
+
+  if (t_beg < t_end) issue(t_beg);
+  for (int t = t_beg; t < t_end; ++t) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (t + 1 < t_end) issue(t + 1);
+#pragma unroll
+    for (int s = wk; s < KSTEPS; s += KSPLIT) {
+      const int px0 = 32 * s + 4 * gq + q, px1 = px0 + 16;   // rows of read 0 / read 1
+      bf16x8w a[NP][2];
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+          a[i][f] = tr_frag(gimg + i * GY_PIECE + px0 * GSB + acol + f * 32,
+                            gimg + i * GY_PIECE + px1 * GSB + acol + f * 32);
+      int hp0, hp1;
+      {
+        const int im0 = px0 / T::IPX, rm0 = px0 % T::IPX;
+        const int im1 = px1 / T::IPX, rm1 = px1 % T::IPX;
+        hp0 = (im0 * T::HP + rm0 / TW) * T::WP + rm0 % TW;
+        hp1 = (im1 * T::HP + rm1 / TW) * T::WP + rm1 % TW;
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = (tap / 3) * T::WP + tap % 3;
+        bf16x8w b[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+          b[i] = tr_frag(aimg + i * ACT_PIECE + (hp0 + toff) * WGS_ASB + bcol,
+                         aimg + i * ACT_PIECE + (hp1 + toff) * WGS_ASB + bcol);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          f32x4 c = acc[f][tap];
+          if (NP == 3) {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][f], b[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[NP - 1][f], b[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][f], b[NP - 1], c, 0, 0, 0);
+          }
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][f], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][f], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][f], b[0], c, 0, 0, 0);
+          acc[f][tap] = c;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (KSPLIT == 2) {   // fold the second K half into the first through LDS
+    float* xs = reinterpret_cast<float*>(wsm) + (size_t)(wave - 2 * NWCO) * 72 * 64;
+    if (wk == 1) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xs[((f * 9 + tap) * 4 + r) * 64 + lane] = acc[f][tap][r];
+    }
+    __syncthreads();
+    if (wk == 0) {
+      xs = reinterpret_cast<float*>(wsm) + (size_t)wave * 72 * 64;
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[f][tap][r] += xs[((f * 9 + tap) * 4 + r) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  // partial layout [slice][tap][co][ci]; 16x16 C/D: col = ci (lane & 15), row = co
+  const int ci = ci0 + wci * 16 + (lane & 15);
+  if (wk == 0) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wco * 32 + f * 16 + (lane >> 4) * 4 + r;
+          wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] = acc[f][tap][r];
+        }
+  }
+  if (do_bias) {
+    double* xb = reinterpret_cast<double*>(wsm);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xb[i * 256 + tid] = bs[i];
+    __syncthreads();
+    if (tid < CO_T) {
+      const int qq = tid >> 2, i = tid & 3;
+      double sum = 0.0;
+      for (int m = qq; m < 256; m += QG) sum += xb[i * 256 + m];
+      bpart[(size_t)slice * Cout + co0 + tid] = (float)sum;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ cin == 1 (first conv)
 // taps become the N dimension: B[k=px][j=tap] = x[px + d(tap)] (j < 9), 16x16x4 MFMA.
 __global__ __launch_bounds__(128) void wgrad_cin1_kernel(
@@ -503,9 +773,109 @@ static void launch_wg(dim3 grid, size_t lds, hipStream_t s, const float* src, co
     launch_wg_tw<NWCO, KSPLIT, MODE, 8>(grid, lds, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
 }
 
+template <int NP, int NWCO, int KSPLIT, int MODE, int TW, int PT>
+static void launch_wgs_tw(dim3 grid, hipStream_t s, const float* src, const float* st,
+                          const float* gy, float* wpart, float* bpart, int B, int H, int W, int cin,
+                          int cout, const WgGeom& g) {
+  using T = WgTileP<TW, PT>;
+  constexpr int CO_T = NWCO * 32;
+  const size_t lds_img = (size_t)NP * ((size_t)PT * (CO_T * 2 + 32) + (size_t)T::HALO * WGS_ASB);
+  const size_t lds_fold = KSPLIT == 2 ? (size_t)2 * 72 * 64 * 4 : 0;
+  const size_t lds_bias = 256 * 4 * 8;
+  size_t lds = lds_img;
+  if (lds < lds_fold) lds = lds_fold;
+  if (lds < lds_bias) lds = lds_bias;
+  auto k = wgrad_split_kernel<NP, NWCO, KSPLIT, MODE, TW, PT>;
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, (const float2*)st, gy, wpart, bpart, B, H, W,
+                     cin, cout, g);
+}
+
+template <int NP, int NWCO, int KSPLIT, int MODE>
+static void launch_wgs(dim3 grid, hipStream_t s, const float* src, const float* st, const float* gy,
+                       float* wpart, float* bpart, int B, int H, int W, int cin, int cout,
+                       const WgGeom& g) {
+  constexpr int PT = 64;
+  if (g.TW == 32)
+    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 32, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+  else if (g.TW == 16)
+    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 16, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+  else if constexpr (NWCO == 1)
+    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 8, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+}
+
+template <int NP>
+static void dispatch_wgs(int mode, bool narrow, dim3 grid, hipStream_t s, const float* src,
+                         const float* st, const float* gy, float* wpart, float* bpart, int B, int H,
+                         int W, int cin, int cout, const WgGeom& g) {
+  if (narrow) {
+    switch (mode) {
+      case ACT_RAW: launch_wgs<NP, 1, 2, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_NORM: launch_wgs<NP, 1, 2, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_UP: launch_wgs<NP, 1, 2, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      default: launch_wgs<NP, 1, 2, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+    }
+  } else {
+    switch (mode) {
+      case ACT_RAW: launch_wgs<NP, 2, 1, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_NORM: launch_wgs<NP, 2, 1, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_UP: launch_wgs<NP, 2, 1, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      default: launch_wgs<NP, 2, 1, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+    }
+  }
+}
+
+static bool wgs_geom_ok(const WgGeom& g, int pt) {
+  if (pt == 128)
+    return (g.TW == 32 && g.TH == 4) || (g.TW == 16 && g.TH == 8 && g.NI == 1) ||
+           (g.TW == 8 && g.TH == 8 && g.NI == 2);
+  return (g.TW == 32 && g.TH == 2) || (g.TW == 16 && g.TH == 4 && g.NI == 1) ||
+         (g.TW == 8 && g.TH == 8 && g.NI == 1);
+}
+
 }  // namespace ev
 
 using namespace ev;
+
+extern "C" int ebsdvae_conv3x3_wgrad_split_slices(int B, int H, int W, int cin, int cout, int pieces) {
+  WgGeom g;
+  if (pieces != 2 && pieces != 3) return -1;
+  if (cin % 32 || !(cout == 32 || cout % 64 == 0)) return -1;
+  const int pt = 64;
+  if (!wg_geom(B, H, W, cin, cout, &g, pt) || !wgs_geom_ok(g, pt)) return -1;
+  return g.slices;
+}
+
+extern "C" int ebsdvae_conv3x3_wgrad_split(const float* src, const float* src_stats, int src_mode,
+                                           const float* gy, float* wpart, float* bpart, int B,
+                                           int H, int W, int cin, int cout, int pieces,
+                                           ebsdvae_stream_t stream) {
+  WgGeom g;
+  EV_REQUIRE(src && gy && wpart && bpart && B > 0, "conv3x3_wgrad_split: null pointer");
+  EV_REQUIRE(pieces == 2 || pieces == 3, "conv3x3_wgrad_split: pieces=%d (2 or 3)", pieces);
+  EV_REQUIRE(src_mode >= 0 && src_mode <= 4 && src_mode != ACT_NORM_POOL,
+             "conv3x3_wgrad_split: bad src_mode %d (pool-fed layers pass the pooled activation RAW)",
+             src_mode);
+  EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats, "conv3x3_wgrad_split: NORM needs stats");
+  EV_REQUIRE(cin % 32 == 0 && (cout == 32 || cout % 64 == 0), "conv3x3_wgrad_split: cin=%d cout=%d unsupported",
+             cin, cout);
+  const int pt = 64;   // 64-pixel tiles: the per-piece LDS images and prefetch registers fit
+  EV_REQUIRE(wg_geom(B, H, W, cin, cout, &g, pt) && wgs_geom_ok(g, pt),
+             "conv3x3_wgrad_split: unsupported shape H=%d W=%d", H, W);
+  hipStream_t s = (hipStream_t)stream;
+  // 32-wide co tiles where the 64-wide variant would exceed 256 VGPRs
+  const bool narrow = cout == 32 || g.TW == 8 || (pieces == 3 && g.TW == 16);
+  const dim3 grid(g.slices, narrow ? cout / 32 : cout / 64, cin / 32);
+  if (pieces == 3)
+    dispatch_wgs<3>(src_mode, narrow, grid, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g);
+  else
+    dispatch_wgs<2>(src_mode, narrow, grid, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g);
+  return evh::check_launch("wgrad_split");
+}
 
 extern "C" int ebsdvae_conv3x3_wgrad_slices(int B, int H, int W, int cin, int cout) {
   WgGeom g;

@@ -40,6 +40,8 @@ SIGNATURES = {
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],
     "ebsdvae_conv3x3_wgrad_slices": [I, I, I, I, I],
     "ebsdvae_conv3x3_wgrad": [P, P, I, P, P, P, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_wgrad_split_slices": [I, I, I, I, I, I],
+    "ebsdvae_conv3x3_wgrad_split": [P, P, I, P, P, P, I, I, I, I, I, I, P],
     "ebsdvae_wgrad_reduce_work": [I, I, I],
     "ebsdvae_wgrad_reduce": [P, P, I, P, P, I, I, I, P, P],
     "ebsdvae_in_stats_finalize": [P, P, I, I, I, I, P],
@@ -72,7 +74,7 @@ _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": 
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
            "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
-           "ebsdvae_pack_split_bytes"}
+           "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices"}
 
 _lib = None
 _lock = threading.Lock()

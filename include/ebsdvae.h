@@ -133,6 +133,13 @@ int ebsdvae_conv3x3_wgrad(const float* src, const float* src_stats, int src_mode
                           int cin, int cout, ebsdvae_stream_t stream);
 /* work: device scratch of ebsdvae_wgrad_reduce_work(...) bytes (double partial sums) */
 size_t ebsdvae_wgrad_reduce_work(int slices, int cin, int cout);
+/* Split-bf16 weight gradient (pieces = 2 or 3, as ebsdvae_conv3x3_fwd_split): same partial
+ * layout and reduction as ebsdvae_conv3x3_wgrad, 64-pixel tiles on
+ * v_mfma_f32_16x16x32_bf16 with transposed LDS reads; cin % 32 == 0, cout 32 or 64k. */
+int ebsdvae_conv3x3_wgrad_split_slices(int B, int H, int W, int cin, int cout, int pieces);
+int ebsdvae_conv3x3_wgrad_split(const float* src, const float* src_stats, int src_mode,
+                                const float* gy, float* wpart, float* bpart, int B, int H, int W,
+                                int cin, int cout, int pieces, ebsdvae_stream_t stream);
 int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
                          float* db, int cin, int cout, int kind, void* work,
                          ebsdvae_stream_t stream);

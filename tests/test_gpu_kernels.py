@@ -14,6 +14,14 @@ pytestmark = pytest.mark.gpu
 TOL = 2e-5   # fp32 single-layer ops vs float64
 
 
+@pytest.fixture(autouse=True)
+def _fp32_kernels():
+    """These tests pin the fp32-MFMA kernels; the split-bf16 tests switch precision
+    explicitly inside."""
+    with E.precision("fp32"):
+        yield
+
+
 def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
 
@@ -462,3 +470,34 @@ def test_dgrad_fused_split_bf16(cuda, cin, cout, H, pmode, prec):
         ga = gn
     ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
     assert O.rel_err(host(g_prev), ref) < 2e-4
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("cin,cout,H,mode,kind", [c for c in WG_CASES if c[0] >= 32 and c[1] >= 32])
+def test_conv_wgrad_split_bf16(cuda, cin, cout, H, mode, kind, prec):
+    """Split-bf16 weight gradient == float64 oracle (bf16x3 within 1e-4, bf16x6 at fp32 grade)."""
+    rng = np.random.default_rng(51 + cin + cout + H + mode)
+    B = 3 if H <= 64 else 2
+    s, mean, rstd, st = make_src(rng, B, H, cin, mode)
+    gy = rng.standard_normal((B, H, H, cout))
+    wshape = (cout, cin, 3, 3) if kind == 0 else (cin, cout, 3, 3)
+    dw = torch.empty(wshape, device="cuda")
+    db = torch.empty(cout, device="cuda")
+    old = E.get_precision()
+    E.set_precision(prec)
+    try:
+        if mode == E.ACT_NORM_POOL:
+            layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
+            wdummy = dev(np.zeros((cout, cin, 3, 3)))
+            _, _, act = E.conv_forward(dev(s), dev(st), layer, wdummy, dev(np.zeros(cout)), B, keep_act=True)
+            E.conv_wgrad(act, None, E.ACT_RAW, dev(gy), cin, cout, kind, dw, db)
+        else:
+            E.conv_wgrad(dev(s), dev(st) if mode in (1, 2, 4) else None, mode, dev(gy), cin, cout, kind, dw, db)
+    finally:
+        E.set_precision(old)
+    a = act_oracle(s, mean, rstd, mode)
+    rw, rb = O.conv3x3_wgrad(a, gy)
+    if kind == 1:
+        rw = rw.transpose(1, 0, 2, 3)[:, :, ::-1, ::-1]
+    assert O.rel_err(host(dw), rw) < SPLIT_TOL[prec] * 2
+    assert O.rel_err(host(db), rb) < 5e-5

@@ -42,8 +42,17 @@ def h(t):
     return t.detach().double().cpu().numpy()
 
 
+@pytest.fixture(params=["bf16x6", "fp32"])
+def prec(request):
+    """The model-level gates hold for the default fp32-grade split-bf16 convs AND the pure
+    fp32-MFMA convs."""
+    from latice import engine as E
+    with E.precision(request.param):
+        yield request.param
+
+
 @pytest.mark.parametrize("name", FIXTURES)
-def test_forward_loss_backward_vs_reference(cuda, name):
+def test_forward_loss_backward_vs_reference(cuda, name, prec):
     f = O.load_fixture(os.path.join(GOLDEN, name + ".npz"))
     m = build(f, cuda)
     x = torch.from_numpy(f["x"]).to(cuda)
@@ -119,7 +128,7 @@ def test_lightning_training_step_and_fused_adam(cuda):
     lm.on_train_epoch_end()
 
 
-def test_batch_independence_at_full_size(cuda):
+def test_batch_independence_at_full_size(cuda, prec):
     """B=256 (the bench config): per-sample outputs equal a B=4 run of the same samples
     (InstanceNorm is per sample; size-independent property of the full-size path)."""
     sd = {k: torch.from_numpy(v) for k, v in seeded_state_dict(0).items()}
@@ -140,7 +149,7 @@ def test_batch_independence_at_full_size(cuda):
 
 
 @pytest.mark.parametrize("name", FIXTURES)
-def test_encoder_only_latents_vs_reference(cuda, name):
+def test_encoder_only_latents_vs_reference(cuda, name, prec):
     """encode_mu (the build_dictionary fast path, BASELINE c4) == the reference's mu."""
     f = O.load_fixture(os.path.join(GOLDEN, name + ".npz"))
     m = build(f, cuda)
