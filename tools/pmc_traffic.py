@@ -23,7 +23,11 @@ from collections import defaultdict
 FAMILIES = [
     ("conv3x3_big_kernel", "conv3x3_fwd"),
     ("conv3x3_small_kernel", "conv3x3_fwd"),
+    ("conv3x3_split_kernel", "conv3x3_fwd"),
     ("ev::wgrad_kernel<", "conv3x3_wgrad"),
+    ("wgrad_split_kernel", "conv3x3_wgrad"),
+    ("pack_split", "pack_weight"),
+    ("pack_conv_weights", "pack_weight"),
     ("wgrad_reduce", "wgrad_reduce"),
     ("in_bwd_edge_kernel", "in_bwd_edge"),
     ("in_bwd_kernel", "in_bwd"),
