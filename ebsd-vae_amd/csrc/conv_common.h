@@ -49,7 +49,7 @@ EV_DEVINL void inbwd_acc(float g, const float* v, float2 sp, float& s1, float& s
   s2 = fmaf(ga, x, s2);
 }
 
-template <int MF, int NF, int FP>
+template <int MF, int NF, int FP, int GMAX = 32>
 EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bias,
                              float* __restrict__ y, float2* __restrict__ spart, int B, int H,
                              int W, int Cout, int b0, int h0, int tpx, int wpx0, int co_base,
@@ -80,9 +80,9 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 #endif
       }
     if (FP != FP_NONE && bvalid) {
-      // loads in batches of 32 issued before any use (latency overlapped within a batch)
+      // loads in batches of GMAX values issued before any use (latency overlapped within a batch)
       constexpr int NL = FP == P_POOL ? 4 : 1;
-      constexpr int G = (32 / NL) < MF * 16 ? (32 / NL) : MF * 16;
+      constexpr int G = (GMAX / NL) < MF * 16 ? (GMAX / NL) : MF * 16;
       static_assert((MF * 16) % G == 0, "batch size");
       const int lW = 31 - __builtin_clz(W);
       const size_t plane = FP == P_POOL ? (size_t)4 * H * W : (FP == P_UP ? (size_t)(H * W) / 4 : (size_t)H * W);

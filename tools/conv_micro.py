@@ -1,0 +1,130 @@
+"""Stand-alone timing of single conv launches through the C ABI (HIP events, one stream),
+for kernel A/B work and short rocprofv3 --pmc passes.
+
+    python tools/conv_micro.py [--reps 20] [--pieces 3] [--only fwd32]
+
+Cases are the training step's dominant shapes at B=256: each prints
+the average launch time and the algorithmic fp32-equivalent TFLOP/s.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ebsd-vae_amd")]
+
+import torch  # noqa: E402
+
+from latice import _native as N  # noqa: E402
+from latice.engine import ACT_NORM, ACT_NORM_POOL, ACT_NORM_UP, P_ID, P_POOL  # noqa: E402
+
+# name: (kind, H, cin, cout, src_mode / pmode)
+CASES = {
+    "fwd32": ("fwd", 128, 32, 32, ACT_NORM),
+    "fwd64": ("fwd", 64, 64, 64, ACT_NORM),
+    "fwd128": ("fwd", 32, 128, 128, ACT_NORM),
+    "fwd128s16": ("fwd", 16, 128, 128, ACT_NORM),
+    "fwd32to64p": ("fwd", 64, 32, 64, ACT_NORM_POOL),
+    "fwd64to32u": ("fwd", 128, 64, 32, ACT_NORM_UP),
+    "dgrad32": ("dgrad", 128, 32, 32, P_ID),
+    "dgrad64": ("dgrad", 64, 64, 64, P_ID),
+    "wgrad32": ("wgrad", 128, 32, 32, ACT_NORM),
+    "wgrad64": ("wgrad", 64, 64, 64, ACT_NORM),
+    "wgrad128": ("wgrad", 32, 128, 128, ACT_NORM),
+}
+
+
+def run(name, reps, pieces, B):
+    kind, H, cin, cout, mode = CASES[name]
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    s = N.stream()
+    flops = 2.0 * B * H * H * cin * cout * 9
+    w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) * 0.05
+    bias = torch.zeros(cout, device=dev)
+    if kind == "fwd":
+        Hs = 2 * H if mode == ACT_NORM_POOL else (H // 2 if mode == ACT_NORM_UP else H)
+        src = torch.randn(B, Hs, Hs, cin, device=dev, generator=g)
+        st = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
+        wp = torch.empty(N.call("ebsdvae_pack_split_bytes", cin, cout, pieces) // 4, device=dev)
+        d = (N.PackDesc * 1)(N.PackDesc(w.data_ptr(), wp.data_ptr(), cin, cout, 0, 0))
+        N.call("ebsdvae_pack_conv_weights_split", ctypes.addressof(d), 1, pieces, s)
+        y = torch.empty(B, H, H, cout, device=dev)
+        T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, H, cout)
+        part = torch.empty(B, T, cout, 2, device=dev)
+
+        def launch():
+            N.call("ebsdvae_conv3x3_fwd_split", src.data_ptr(), st.data_ptr(), mode, wp.data_ptr(),
+                   bias.data_ptr(), y.data_ptr(), part.data_ptr(), None, B, H, H, cin, cout, pieces, s)
+    elif kind == "dgrad":
+        # input gradient of a cin->cout layer: a conv cout->cin, fused reduce of the block
+        # feeding it (y_prev at 2H for P_POOL)
+        gy = torch.randn(B, H, H, cout, device=dev, generator=g)
+        Hp = 2 * H if mode == P_POOL else H
+        yprev = torch.randn(B, Hp, Hp, cin, device=dev, generator=g)
+        stp = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
+        wp = torch.empty(N.call("ebsdvae_pack_split_bytes", cout, cin, pieces) // 4, device=dev)
+        d = (N.PackDesc * 1)(N.PackDesc(w.data_ptr(), wp.data_ptr(), cin, cout, 0, 1))
+        N.call("ebsdvae_pack_conv_weights_split", ctypes.addressof(d), 1, pieces, s)
+        gin = torch.empty(B, H, H, cin, device=dev)
+        T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, H, cin)
+        part = torch.empty(B, T, cin, 2, dtype=torch.float64, device=dev)
+
+        def launch():
+            N.call("ebsdvae_conv3x3_dgrad_inbwd_split", gy.data_ptr(), wp.data_ptr(), gin.data_ptr(),
+                   yprev.data_ptr(), stp.data_ptr(), mode, part.data_ptr(), B, H, H, cout, cin, pieces, s)
+    else:
+        src = torch.randn(B, H, H, cin, device=dev, generator=g)
+        st = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
+        gy = torch.randn(B, H, H, cout, device=dev, generator=g)
+        S_ = N.call("ebsdvae_conv3x3_wgrad_split_slices", B, H, H, cin, cout, pieces)
+        wpart = torch.empty(S_, 9, cout, cin, device=dev)
+        bpart = torch.empty(S_, cout, device=dev)
+
+        def launch():
+            N.call("ebsdvae_conv3x3_wgrad_split", src.data_ptr(), st.data_ptr(), mode, gy.data_ptr(),
+                   wpart.data_ptr(), bpart.data_ptr(), B, H, H, cin, cout, pieces, s)
+    for _ in range(3):
+        launch()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    lib = N.load()
+    if hasattr(lib, "ebsdvae_debug_pipe_trace"):   # EV_PIPE_TRACE build: per-wave cycle split
+        import numpy as np
+        buf = np.zeros(4096 * 8 * 6, dtype=np.uint64)
+        lib.ebsdvae_debug_pipe_trace(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(buf.nbytes))
+        t = buf.reshape(4096, 8, 6).astype(np.float64)
+        t = t[t[:, 0, 0] > 0]
+        tot = t[:, :, 0].mean()
+        print(f"   trace ({len(t)} blocks, {t[0, 0, 5]:.0f} iters): total {tot:.0f} cyc; issue "
+              f"{t[:, :, 1].mean() / tot:.3f} kloop {t[:, :, 2].mean() / tot:.3f} barrier "
+              f"{t[:, :, 3].mean() / tot:.3f} epilogue {t[:, :, 4].mean() / tot:.3f}; per-wave barrier "
+              + " ".join(f"{v:.2f}" for v in (t[:, :, 3].mean(0) / tot)))
+    peak = 2516.6 / {2: 3, 3: 6}[pieces]
+    tf = flops / us / 1e6
+    print(f"{name:12s} {kind:5s} {cin:3d}->{cout:3d} @{H:3d}  {us:8.1f} us  {tf:6.1f} TF/s  "
+          f"{tf / peak:5.3f} of peak", flush=True)
+    return us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--pieces", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    names = [n for n in CASES if not a.only or n in a.only.split(",")]
+    for n in names:
+        run(n, a.reps, a.pieces, a.batch)
+
+
+if __name__ == "__main__":
+    main()
