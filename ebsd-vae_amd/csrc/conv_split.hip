@@ -47,7 +47,7 @@ constexpr int XCK = 8;      // input channels per chunk
 constexpr int XTAPS = 10;   // 9 taps + one zero tap
 constexpr int XPS = 48;     // halo pixel record (bytes)
 #ifndef EV_PIPE_EPI_G
-#define EV_PIPE_EPI_G 8   // fused IN-backward loads in flight per batch (VGPR budget)
+#define EV_PIPE_EPI_G 8   // fused IN-backward loads in flight per batch, NF > 1 (VGPR budget)
 #endif
 
 // x -> NP bf16 pieces (the remainder is re-split exactly in fp32 at every step)
@@ -277,6 +277,21 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_split_kernel(
                             l32, yprev, stprev, ipart);
 }
 
+// Workgroup barrier that leaves this wave's N youngest vector-memory operations in flight:
+// s_waitcnt vmcnt(N) lgkmcnt(0); s_barrier.  The empty asm "memory" clobbers keep the
+// compiler from moving LDS / global accesses across it.
+// 1-KiB LDS-DMA pieces per wave and chunk of the pipelined kernel's weight slab
+constexpr int pipe_dma_per(int wslab, int nwv) { return (wslab / 1024 + nwv - 1) / nwv; }
+
+template <int N>
+EV_DEVINL void pipe_barrier() {
+  static_assert(N >= 0 && N < 16, "vmcnt range");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(N | (7 << 4));   // vmcnt(N) expcnt(7) lgkmcnt(0) (gfx9 encoding)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Epilogue of conv3x3_pipe_kernel: conv_epilogue (conv_common.h) for one tile of one image,
 // with 32-bit buffer offsets instead of 64-bit addresses (the same values, the same
 // summation order, so results are bit-identical to the non-persistent kernel's).
@@ -309,7 +324,8 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
       }
     if (FP != FP_NONE) {
       constexpr int NL = FP == P_POOL ? 4 : 1;
-      constexpr int G = (EV_PIPE_EPI_G / NL) < MF * 16 ? (EV_PIPE_EPI_G / NL) : MF * 16;
+      constexpr int GM = NF == 1 ? 32 : EV_PIPE_EPI_G;   // loads in flight per batch
+      constexpr int G = (GM / NL) < MF * 16 ? (GM / NL) : MF * 16;
       static_assert((MF * 16) % G == 0, "batch size");
       const int lW = 31 - __builtin_clz(W);
       const int plane = FP == P_POOL ? 4 * H * W : (FP == P_UP ? (H * W) / 4 : H * W);
@@ -383,17 +399,20 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr int MW = MF * 32;
   constexpr int NTHR = NWV * 64;
   constexpr int WSLAB = XTAPS * NP * NT * 16;
+  constexpr int WPER = pipe_dma_per(WSLAB, NWV);  // 1-KiB weight pieces per wave per chunk
+  constexpr int WSLABP = WPER * NWV * 1024;       // LDS weight buffer (padded to whole rounds)
   constexpr bool POOL = (MODE == ACT_NORM_POOL);
   constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_POOL || MODE == ACT_NORM_UP);
   constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
   constexpr int NR = POOL ? 4 : 1;
   constexpr int PD = POOL ? 1 : 2;               // halo prefetch distance (iterations)
+  static_assert(PD == 1 || KX * NR <= 7, "pipe_barrier keeps at most 7 loads in flight");
   extern __shared__ __attribute__((aligned(16))) char xsm[];
   const int HP = TH + 2, WP = W + 2;
   const int pixP = HP * WP;
   const int xslab = (pixP + 1) * XPS;
   char* lw0 = xsm;
-  char* lx0 = xsm + 2 * WSLAB;
+  char* lx0 = xsm + 2 * WSLABP;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -439,9 +458,16 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     else o = r * rowb + c * Cin * 4;
     hm1[k] = in ? r : -(1 << 28);
     boff[k] = in ? o + q * 16 : (int)0x80000000;
+#ifdef EV_X_CONTIG   // timing experiment only: contiguous halo bytes (wrong results)
+    boff[k] = in ? (pix * 32 + q * 16) : (int)0x80000000;
+#endif
     ldo[k] = (pix < pixP ? pix : pixP) * XPS + q * 8;
   }
   const int img_bytes = Hs * Ws * Cin * 4;
+  // item k of this wave holds at least one halo pixel (wave index made provably uniform so
+  // the test is a scalar branch)
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto item_live = [&](int k) EV_LAMBDA_INLINE { return (wave_u * 64 + NTHR * k) < 2 * pixP; };
 
   float4 raw[PD][KX][NR];
   float2 st[PD][4];
@@ -465,7 +491,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     sb0[sl] = b0; sh0[sl] = h0; sch[sl] = ch;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)b0 * Hs * Ws * Cin), 0,
                                                       img_bytes, 0x00020000);
+#ifdef EV_X_CONTIG
+    const int toff = h0 * rowb + ch * (pixP * 32);
+#else
     const int toff = (POOL ? 2 * h0 : (UPS ? (h0 >> 1) : h0)) * rowb + ch * XCK * 4;
+#endif
     int m = 0;
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
@@ -482,10 +512,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     }
     okm[sl] = m;
     if (NORM) {
-      const auto rst = __builtin_amdgcn_make_buffer_rsrc((void*)(sstats + (size_t)b0 * Cin), 0, Cin * 8,
-                                                         0x00020000);
-      const float4 s01 = bload4(rst, (ch * XCK + q * 4) * 8);
-      const float4 s23 = bload4(rst, (ch * XCK + q * 4) * 8 + 16);
+      // the chunk's 8 {mean, rstd} pairs are wave-uniform: one scalar-cache load (no TA
+      // traffic), then each lane keeps its 4-channel half
+      const float4* sp = reinterpret_cast<const float4*>(sstats + (size_t)b0 * Cin + ch * XCK);
+      const float4 u0 = sp[0], u1 = sp[1], u2 = sp[2], u3 = sp[3];
+      const float4 s01 = q ? u2 : u0, s23 = q ? u3 : u1;
       st[sl][0] = make_float2(s01.x, s01.y); st[sl][1] = make_float2(s01.z, s01.w);
       st[sl][2] = make_float2(s23.x, s23.y); st[sl][3] = make_float2(s23.z, s23.w);
     }
@@ -519,12 +550,18 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) fs[i] = NORM ? norm_fs(st[sl][i]) : make_float2(1.f, 0.f);
   };
+  // weight slab DMA: every wave issues exactly WPER 1-KiB pieces per chunk (the padding
+  // pieces of the last chunk fall outside the descriptor's range), so every iteration issues
+  // the same, compile-time number of vector-memory ops and the compiler's waits stay exact
+  const auto rwp = __builtin_amdgcn_make_buffer_rsrc((void*)wp, 0, nch * WSLAB, 0x00020000);
   auto issue_weights = [&](int it, char* lw) EV_LAMBDA_INLINE {
     const int ch = it - (it / nch) * nch;
-    const char* g = wp + (size_t)ch * WSLAB;
-    for (int pc = wave; pc < WSLAB / 1024; pc += NWV)
-      __builtin_amdgcn_global_load_lds((const void*)(g + pc * 1024 + lane * 16),
-                                       (lds_void_ptr)(lw + pc * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < WPER; ++j) {
+      const int pc = wave_u + j * NWV;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwp, (lds_void_ptr)(lw + pc * 1024), 16,
+                                               ch * WSLAB + pc * 1024 + lane * 16, 0, 0, 0);
+    }
   };
 
   f32x16 acc[MF][NF];
@@ -547,6 +584,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #ifdef EV_PIPE_TRACE
   unsigned long long tr_issue = 0, tr_k = 0, tr_bar = 0, tr_epi = 0;
   const unsigned long long tr_start = __builtin_amdgcn_s_memtime();
+  const unsigned long long tr_rstart = __builtin_amdgcn_s_memrealtime();
 #endif
   // one pipelined iteration; P = it & 1 selects the LDS buffers and register slots statically
   auto body = [&](int it, auto P_c) EV_LAMBDA_INLINE {
@@ -554,15 +592,17 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     constexpr int SL_LD = PD == 2 ? P : 0;        // slot receiving it+PD
     constexpr int SL_ST = PD == 2 ? 1 - P : 0;    // slot holding it+1
     EV_T(tb0);
-    const bool more1 = it + 1 < nit;
-    if (more1) issue_weights(it + 1, lw0 + (1 - P) * WSLAB);
-    if (it + PD < nit) issue_halo(it + PD, std::integral_constant<int, SL_LD>());
+    // unconditional issue (indices clamped at the end: the surplus loads land in buffers
+    // nobody reads), so every iteration has the same vector-memory op count
+    const int it1 = min(it + 1, nit - 1), itp = min(it + PD, nit - 1);
+    issue_weights(it1, lw0 + (1 - P) * WSLABP);
+    issue_halo(itp, std::integral_constant<int, SL_LD>());
     EV_TACC(tr_issue, tb0);
     EV_T(tb1);
     float2 fs[4];
-    if (more1) stage_fs(std::integral_constant<int, SL_ST>(), fs);
+    stage_fs(std::integral_constant<int, SL_ST>(), fs);
     const char* lx = lx0 + P * xslab;
-    const char* lw = lw0 + P * WSLAB;
+    const char* lw = lw0 + P * WSLABP;
     char* lxn = lx0 + (1 - P) * xslab;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
@@ -595,18 +635,23 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
         }
       // staging of it+1, spread over the k-steps (PD = 1: its loads were issued this
       // iteration, so stage after the last k-step's MFMAs are queued)
-      if (more1) {
 #pragma unroll
-        for (int k = 0; k < KX; ++k)
-          if ((PD == 2 ? (k * 5) / KX : 4) == s) stage_item(std::integral_constant<int, SL_ST>(), k, fs, lxn);
-      }
+      for (int k = 0; k < KX; ++k)
+        if ((PD == 2 ? (k * 5) / KX : 4) == s && item_live(k))
+          stage_item(std::integral_constant<int, SL_ST>(), k, fs, lxn);
 #ifndef EV_PIPE_NO_SCHED_FENCE
       __builtin_amdgcn_sched_barrier(0);   // one scheduling region per k-step (VGPR budget)
 #endif
     }
     EV_TACC(tr_k, tb1);
     EV_T(tb2);
-    __syncthreads();
+    if (PD == 2) {
+      // the halo loads of it+2 (this wave's youngest vector-memory ops) stay in flight across
+      // the barrier: everything older -- the weight DMA of it+1, epilogue traffic -- is retired
+      pipe_barrier<(PD == 2 ? KX * NR : 0)>();
+    } else {
+      __syncthreads();
+    }
     EV_TACC(tr_bar, tb2);
   };
 
@@ -622,9 +667,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   {
     float2 fs[4];
     stage_fs(std::integral_constant<int, 0>(), fs);
-    if (PD == 2 && nit > 1) issue_halo(1, std::integral_constant<int, PD == 2 ? 1 : 0>());
+    if (PD == 2) issue_halo(min(1, nit - 1), std::integral_constant<int, PD == 2 ? 1 : 0>());
 #pragma unroll
-    for (int k = 0; k < KX; ++k) stage_item(std::integral_constant<int, 0>(), k, fs, lx0);
+    for (int k = 0; k < KX; ++k)
+      if (item_live(k)) stage_item(std::integral_constant<int, 0>(), k, fs, lx0);
   }
   __syncthreads();
   // nch = Cin / 8 is even for every supported layer (plan_split), so it & 1 == ch & 1
@@ -643,7 +689,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   if (lane == 0 && blockIdx.x < 4096) {
     unsigned long long* o = ev_pipe_trace + ((size_t)blockIdx.x * 8 + (wave & 7)) * 6;
     o[0] = __builtin_amdgcn_s_memtime() - tr_start;
-    o[1] = tr_issue; o[2] = tr_k; o[3] = tr_bar; o[4] = tr_epi; o[5] = nit;
+    o[1] = tr_issue; o[2] = tr_k; o[3] = tr_bar; o[4] = tr_epi;
+    o[5] = __builtin_amdgcn_s_memrealtime() - tr_rstart;   // 100 MHz
   }
 #endif
 }
@@ -708,7 +755,8 @@ static int cu_count() {
 
 struct X3Cfg {
   int M, TH, NT, KX, nwv;
-  size_t lds;
+  size_t lds;        // conv3x3_split_kernel
+  size_t lds_pipe;   // conv3x3_pipe_kernel (padded weight buffers); 0 = does not fit
 };
 
 // NP = 2: Cout 128 -> 8 waves x M 256; Cout 64 / 32 -> 4 waves x M 256 (2 blocks / CU).
@@ -726,7 +774,10 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   c->KX = (pix * 2 + c->nwv * 64 - 1) / (c->nwv * 64);
   const int kxmax = np == 2 ? (cout == 128 ? 2 : (cout == 64 ? 5 : 7)) : (cout == 128 ? 2 : (cout == 64 ? 4 : 5));
   if (c->KX > kxmax) return false;
-  c->lds = 2 * (size_t)XTAPS * np * cout * 16 + 2 * (size_t)(pix + 1) * XPS;
+  const int wslab = XTAPS * np * cout * 16;
+  c->lds = 2 * (size_t)wslab + 2 * (size_t)(pix + 1) * XPS;
+  c->lds_pipe = 2 * (size_t)pipe_dma_per(wslab, c->nwv) * c->nwv * 1024 + 2 * (size_t)(pix + 1) * XPS;
+  if (c->lds_pipe > 160 * 1024) c->lds_pipe = 0;
   return c->lds <= 160 * 1024;
 }
 
@@ -735,7 +786,7 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
                         const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                         int cin, hipStream_t s, const InBwdFuse& f) {
   const int ntiles = B * (H / c.TH);
-  if (use_pipe()) {
+  if (use_pipe() && c.lds_pipe) {
     auto k = conv3x3_pipe_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP>;
     static bool once = false;
     if (!once) {
@@ -746,7 +797,7 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
     const int ncu = cu_count();
     const int tpb = (ntiles + ncu - 1) / ncu;
     const int nblk = (ntiles + tpb - 1) / tpb;
-    hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), c.lds, s, src, (const float2*)st,
+    hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), c.lds_pipe, s, src, (const float2*)st,
                        (const char*)wp, bias, y, (float2*)part, aout, B, H, W, cin, c.TH, tpb, f.yprev,
                        f.stprev, f.part);
     return;

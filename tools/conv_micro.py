@@ -10,6 +10,7 @@ import argparse
 import ctypes
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ebsd-vae_amd")]
@@ -35,7 +36,7 @@ CASES = {
 }
 
 
-def run(name, reps, pieces, B):
+def run(name, reps, pieces, B, warm=1.0):
     kind, H, cin, cout, mode = CASES[name]
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -87,6 +88,12 @@ def run(name, reps, pieces, B):
                    wpart.data_ptr(), bpart.data_ptr(), B, H, H, cin, cout, pieces, s)
     for _ in range(3):
         launch()
+    torch.cuda.synchronize()
+    t_end = time.time() + warm   # DVFS: let the clock settle under back-to-back launches
+    while time.time() < t_end:
+        for _ in range(10):
+            launch()
+        torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -103,7 +110,8 @@ def run(name, reps, pieces, B):
         t = buf.reshape(4096, 8, 6).astype(np.float64)
         t = t[t[:, 0, 0] > 0]
         tot = t[:, :, 0].mean()
-        print(f"   trace ({len(t)} blocks, {t[0, 0, 5]:.0f} iters): total {tot:.0f} cyc; issue "
+        clk = (t[:, :, 0] / (t[:, :, 5] / 100.0)).mean() / 1e3
+        print(f"   trace ({len(t)} blocks, clock {clk:.2f} GHz): total {tot:.0f} cyc; issue "
               f"{t[:, :, 1].mean() / tot:.3f} kloop {t[:, :, 2].mean() / tot:.3f} barrier "
               f"{t[:, :, 3].mean() / tot:.3f} epilogue {t[:, :, 4].mean() / tot:.3f}; per-wave barrier "
               + " ".join(f"{v:.2f}" for v in (t[:, :, 3].mean(0) / tot)))
@@ -120,10 +128,11 @@ def main():
     ap.add_argument("--pieces", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--only", default="")
+    ap.add_argument("--warm", type=float, default=1.0, help="seconds of untimed launches first")
     a = ap.parse_args()
     names = [n for n in CASES if not a.only or n in a.only.split(",")]
     for n in names:
-        run(n, a.reps, a.pieces, a.batch)
+        run(n, a.reps, a.pieces, a.batch, a.warm)
 
 
 if __name__ == "__main__":
