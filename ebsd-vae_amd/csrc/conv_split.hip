@@ -595,8 +595,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     // unconditional issue (indices clamped at the end: the surplus loads land in buffers
     // nobody reads), so every iteration has the same vector-memory op count
     const int it1 = min(it + 1, nit - 1), itp = min(it + PD, nit - 1);
+#ifndef EV_PIPE_LATE_ISSUE
     issue_weights(it1, lw0 + (1 - P) * WSLABP);
     issue_halo(itp, std::integral_constant<int, SL_LD>());
+#endif
     EV_TACC(tr_issue, tb0);
     EV_T(tb1);
     float2 fs[4];
@@ -633,6 +635,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
           acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mf], b[1][nf], acc[mf][nf], 0, 0, 0);
           acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mf], b[0][nf], acc[mf][nf], 0, 0, 0);
         }
+#ifdef EV_PIPE_LATE_ISSUE
+      if (s == 0) {   // behind the first k-step's MFMAs, so the matrix pipe covers the issue
+        issue_weights(it1, lw0 + (1 - P) * WSLABP);
+        issue_halo(itp, std::integral_constant<int, SL_LD>());
+      }
+#endif
       // staging of it+1, spread over the k-steps (PD = 1: its loads were issued this
       // iteration, so stage after the last k-step's MFMAs are queued)
 #pragma unroll

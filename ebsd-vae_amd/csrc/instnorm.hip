@@ -30,6 +30,7 @@ __global__ __launch_bounds__(256) void in_stats_finalize_kernel(const float2* __
   const float2* p = part + (size_t)b * T * C + c;
   float m = 0.f;
   int cnt = 0;
+#pragma unroll 8
   for (int t = j; t < T; t += J) { m += p[(size_t)t * C].x; ++cnt; }
   sm[0][tid] = m;
   sm[1][tid] = (float)cnt;
@@ -38,6 +39,7 @@ __global__ __launch_bounds__(256) void in_stats_finalize_kernel(const float2* __
   for (int k = 0; k < J; ++k) mean += sm[0][k * C + c];
   mean /= (float)T;
   float m2 = 0.f, dm = 0.f;
+#pragma unroll 8
   for (int t = j; t < T; t += J) {
     const float2 v = p[(size_t)t * C];
     m2 += v.y;
@@ -128,6 +130,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
     const int W2 = W >> 1, H2 = H >> 1;
     const int q0 = tile * (rows >> 1) * W2, q1 = q0 + (rows >> 1) * W2;
     const float* gnb = gnext + (size_t)b * H2 * W2 * C;
+#pragma unroll 2
     for (int q = q0 + pr; q < q1; q += NPR) {
       const int h2 = q / W2, w2 = q - h2 * W2;
       const float4 g4 = ld4(gnb + (size_t)q * C + c);
@@ -182,6 +185,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
     }
   } else {
     const int p0 = tile * rows * W, p1 = p0 + rows * W;
+#pragma unroll 4
     for (int p = p0 + pr; p < p1; p += NPR) {
       float4 g4;
       if (pmode == P_ID) {
@@ -243,6 +247,7 @@ __global__ __launch_bounds__(256) void in_bwd_finalize_kernel(const double2* __r
   const double2* p = part + (size_t)b * T * C + c;
   double s1 = 0.0, s2 = 0.0;
   if (j < J) {
+#pragma unroll 8
     for (int t = j; t < T; t += J) {
       const double2 v = p[(size_t)t * C];
       s1 += v.x;
@@ -317,19 +322,28 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
 #pragma unroll
     for (int t = 0; t < 9; ++t) wacc[k][t] = 0.f;
   const float* yb = y + (size_t)b * H * W * C;
-  const float* gb1 = gsrc + (size_t)b * H * W;   // FINAL: g1 (1 channel)
-  const float* xb = (FUSE == FUSE_FIRST) ? x + (size_t)b * H * W : nullptr;
+  // the 1-channel neighbour source (FINAL: g1, FIRST: x) of this row band plus its 1-pixel
+  // halo, staged once in LDS with coalesced loads (zero padding at the image border)
+  const float* src1 = ((FUSE == FUSE_FINAL) ? gsrc : x) + (size_t)b * H * W;
+  extern __shared__ float nbs[];   // (rows + 2) x (W + 2)
+  const int r0 = tile * rows, WP = W + 2;
+  for (int i = tid; i < (rows + 2) * WP; i += 256) {
+    const int r = i / WP, cc = i - r * WP;
+    const int gh = r0 - 1 + r, gw = cc - 1;
+    nbs[i] = (gh >= 0 && gh < H && gw >= 0 && gw < W) ? src1[gh * W + gw] : 0.f;
+  }
+  __syncthreads();
   const int p0 = tile * rows * W, p1 = p0 + rows * W;
+#pragma unroll 2
   for (int p = p0 + pr; p < p1; p += NPR) {
     const int h = p / W, w = p - h * W;
     float nb[9];   // FINAL: g1[q - d(tap)] ; FIRST: x[p + d(tap)]
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int kh = t / 3, kw = t % 3;
-      const int hh = (FUSE == FUSE_FINAL) ? h + 1 - kh : h + kh - 1;
-      const int ww = (FUSE == FUSE_FINAL) ? w + 1 - kw : w + kw - 1;
-      const bool ok = hh >= 0 && hh < H && ww >= 0 && ww < W;
-      nb[t] = ok ? ((FUSE == FUSE_FINAL) ? gb1[hh * W + ww] : xb[hh * W + ww]) : 0.f;
+      const int lr = (FUSE == FUSE_FINAL) ? h - r0 + 2 - kh : h - r0 + kh;
+      const int lc = (FUSE == FUSE_FINAL) ? w + 2 - kw : w + kw;
+      nb[t] = nbs[lr * WP + lc];
     }
     float ga[4];
     if (FUSE == FUSE_FINAL) {
@@ -435,6 +449,9 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
   }
 }
 
+// dynamic LDS of in_bwd_edge_kernel: the 1-channel source of one row band + halo
+static size_t edge_lds(int H, int W, int T) { return (size_t)(H / T + 2) * (W + 2) * sizeof(float); }
+
 static int grid_for(size_t n4) {
   size_t g = (n4 + 255) / 256;
   if (g > 8192) g = 8192;
@@ -523,7 +540,7 @@ extern "C" int ebsdvae_in_bwd_final_reduce(const float* g1, const float* w14, co
   EV_REQUIRE(g1 && w14 && y && stats && part && wpart && bpart && C == 32,
              "in_bwd_final_reduce: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, false>), dim3(T, B), dim3(256), 0,
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, false>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)nullptr,
                      (const float*)nullptr, (double2*)part, wpart, bpart, (float*)nullptr, H, W, T);
   return evh::check_launch("in_bwd_final_reduce");
@@ -535,7 +552,7 @@ extern "C" int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, con
   EV_REQUIRE(g1 && w14 && y && stats && bstats && gy && C == 32,
              "in_bwd_final_apply: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), 0,
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)bstats,
                      (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
                      H, W, T);
@@ -549,7 +566,7 @@ extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float*
   EV_REQUIRE(gnext && y && stats && bstats && x && wpart && bpart && C == 32,
              "in_bwd_first_apply_wgrad: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true>), dim3(T, B), dim3(256), 0,
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, gnext, (const float*)nullptr, y, (const float2*)stats,
                      (const float2*)bstats, x, (double2*)nullptr, wpart, bpart, (float*)nullptr, H, W,
                      T);
