@@ -731,6 +731,73 @@ __global__ void wgrad_reduce2_kernel(const double* __restrict__ work, int G, flo
   }
 }
 
+// batched reduction: blockIdx.z = layer (descriptor array passed by value)
+// batched reduction: blockIdx.x runs over every layer's element blocks back to back
+// (blk0[i] = first block of layer i), so small layers cost no idle blocks
+struct WgReduceBatch {
+  ebsdvae_wgrad_reduce_desc d[EBSDVAE_MAX_WGRAD_BATCH];
+  size_t work_off[EBSDVAE_MAX_WGRAD_BATCH];   // in doubles
+  int G[EBSDVAE_MAX_WGRAD_BATCH];
+  int blk0[EBSDVAE_MAX_WGRAD_BATCH + 1];     // level-2 element blocks
+  int r1blk0[EBSDVAE_MAX_WGRAD_BATCH + 1];   // level-1 (slice group x element) blocks
+  int n;
+};
+
+EV_DEVINL int wg_layer_of(const WgReduceBatch& rb, int blk) {
+  int i = 0;
+  while (i + 1 < rb.n && blk >= rb.blk0[i + 1]) ++i;
+  return i;
+}
+
+// level 1: blockIdx.x runs over (layer, slice group g, element block) with no idle blocks:
+// layer L owns blocks [r1blk0[L], r1blk0[L+1]), G[L] x eblocks of them
+__global__ void wgrad_reduce1_batch_kernel(const WgReduceBatch rb, double* __restrict__ work) {
+  int L = 0;
+  while (L + 1 < rb.n && (int)blockIdx.x >= rb.r1blk0[L + 1]) ++L;
+  const ebsdvae_wgrad_reduce_desc& q = rb.d[L];
+  const int G = rb.G[L];
+  const int nw = 9 * q.cin * q.cout, E = nw + q.cout;
+  const int eb = (E + 255) / 256;
+  const int r = blockIdx.x - rb.r1blk0[L];
+  const int g = r / eb;
+  const int e = (r - g * eb) * blockDim.x + threadIdx.x;
+  if (g >= G || e >= E) return;
+  const int S = q.slices;
+  const int k0 = (int)((long)g * S / G), k1 = (int)((long)(g + 1) * S / G);
+  double s = 0.0;
+  if (e < nw) {
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) s += (double)q.wpart[(size_t)k * nw + e];
+  } else {
+    const int co = e - nw;
+    for (int k = k0; k < k1; ++k) s += (double)q.bpart[(size_t)k * q.cout + co];
+  }
+  work[rb.work_off[L] + (size_t)g * E + e] = s;
+}
+
+__global__ void wgrad_reduce2_batch_kernel(const WgReduceBatch rb, const double* __restrict__ work) {
+  const int L = wg_layer_of(rb, blockIdx.x);
+  const ebsdvae_wgrad_reduce_desc& q = rb.d[L];
+  const int G = rb.G[L];
+  const int cin = q.cin, cout = q.cout;
+  const int nw = 9 * cout * cin, E = nw + cout;
+  const int e = (blockIdx.x - rb.blk0[L]) * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const double* w = work + rb.work_off[L];
+  double s = 0.0;
+  for (int g = 0; g < G; ++g) s += w[(size_t)g * E + e];
+  if (e < nw) {
+    const int t = e / (cout * cin), rem = e - t * (cout * cin);
+    const int co = rem / cin, ci = rem - co * cin;
+    size_t idx;
+    if (q.kind == 0) idx = ((size_t)co * cin + ci) * 9 + t;
+    else idx = ((size_t)ci * cout + co) * 9 + (8 - t);
+    q.dw[idx] = (float)s;
+  } else if (q.db) {
+    q.db[e - nw] = (float)s;
+  }
+}
+
 static int reduce_groups(int slices, int cin, int cout) {
   const int E = 9 * cin * cout + cout;
   int G = 524288 / E;
@@ -949,4 +1016,61 @@ extern "C" int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int 
   hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3((E + 255) / 256), dim3(256), 0, st,
                      (const double*)work, G, dw, db, cin, cout, kind);
   return evh::check_launch("wgrad_reduce");
+}
+
+// host-side layout of the batched work buffer (shared by the size query and the launch)
+static bool wg_batch_layout(const ebsdvae_wgrad_reduce_desc* descs, int n, WgReduceBatch* rb,
+                            size_t* total, int* maxE, int* maxG) {
+  size_t off = 0;
+  int blk = 0, blk1 = 0;
+  *maxE = 0;
+  *maxG = 0;
+  for (int i = 0; i < n; ++i) {
+    const ebsdvae_wgrad_reduce_desc& q = descs[i];
+    if (!q.wpart || !q.bpart || !q.dw || q.slices <= 0 || q.cin <= 0 || q.cout <= 0 ||
+        (q.kind != 0 && q.kind != 1))
+      return false;
+    const int E = 9 * q.cin * q.cout + q.cout;
+    const int G = reduce_groups(q.slices, q.cin, q.cout);
+    if (rb) {  // (G may differ per layer; level 1 of layer i uses G[i] groups)
+      rb->d[i] = q;
+      rb->work_off[i] = off;
+      rb->G[i] = G;
+      rb->blk0[i] = blk;
+      rb->r1blk0[i] = blk1;
+    }
+    blk += (E + 255) / 256;
+    blk1 += G * ((E + 255) / 256);
+    off += (size_t)G * E;
+  }
+  if (rb) {
+    rb->blk0[n] = blk;
+    rb->r1blk0[n] = blk1;
+    rb->n = n;
+  }
+  *maxE = blk;    // total level-2 blocks
+  *maxG = blk1;   // total level-1 blocks
+  *total = off * sizeof(double);
+  return true;
+}
+
+extern "C" size_t ebsdvae_wgrad_reduce_batch_work(const ebsdvae_wgrad_reduce_desc* descs, int n) {
+  size_t total = 0;
+  int maxE, maxG;
+  if (!descs || n <= 0 || n > EBSDVAE_MAX_WGRAD_BATCH || !wg_batch_layout(descs, n, nullptr, &total, &maxE, &maxG))
+    return 0;
+  return total;
+}
+
+extern "C" int ebsdvae_wgrad_reduce_batch(const ebsdvae_wgrad_reduce_desc* descs, int n, void* work,
+                                          ebsdvae_stream_t stream) {
+  EV_REQUIRE(descs && work && n > 0 && n <= EBSDVAE_MAX_WGRAD_BATCH, "wgrad_reduce_batch: n=%d out of range", n);
+  WgReduceBatch rb;
+  size_t total = 0;
+  int maxE = 0, maxG = 0;   // total level-2 / level-1 blocks
+  EV_REQUIRE(wg_batch_layout(descs, n, &rb, &total, &maxE, &maxG), "wgrad_reduce_batch: bad descriptor");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wgrad_reduce1_batch_kernel, dim3(maxG), dim3(256), 0, st, rb, (double*)work);
+  hipLaunchKernelGGL(wgrad_reduce2_batch_kernel, dim3(maxE), dim3(256), 0, st, rb, (const double*)work);
+  return evh::check_launch("wgrad_reduce_batch");
 }

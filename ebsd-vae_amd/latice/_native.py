@@ -44,6 +44,8 @@ SIGNATURES = {
     "ebsdvae_conv3x3_wgrad_split": [P, P, I, P, P, P, I, I, I, I, I, I, P],
     "ebsdvae_wgrad_reduce_work": [I, I, I],
     "ebsdvae_wgrad_reduce": [P, P, I, P, P, I, I, I, P, P],
+    "ebsdvae_wgrad_reduce_batch_work": [P, I],
+    "ebsdvae_wgrad_reduce_batch": [P, I, P, P],
     "ebsdvae_in_stats_finalize": [P, P, I, I, I, I, P],
     "ebsdvae_act_apply": [P, P, I, P, I, I, I, I, P],
     "ebsdvae_in_bwd_tiles": [I, I, I],
@@ -69,9 +71,11 @@ SIGNATURES = {
     "ebsdvae_adam": [P, P, P, P, P, P, I64, F, F, F, F, F, I, P],
 }
 _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t,
+            "ebsdvae_wgrad_reduce_batch_work": ctypes.c_size_t,
             "ebsdvae_heads_wgrad_work": ctypes.c_size_t, "ebsdvae_pack_split_bytes": ctypes.c_size_t}
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
+           "ebsdvae_wgrad_reduce_batch_work",
            "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices"}
@@ -87,6 +91,16 @@ class PackDesc(ctypes.Structure):
 
 
 MAX_PACK = 64
+
+
+class WgradReduceDesc(ctypes.Structure):
+    """ebsdvae_wgrad_reduce_desc (include/ebsdvae.h)."""
+    _fields_ = [("wpart", ctypes.c_void_p), ("bpart", ctypes.c_void_p), ("dw", ctypes.c_void_p),
+                ("db", ctypes.c_void_p), ("slices", ctypes.c_int), ("cin", ctypes.c_int),
+                ("cout", ctypes.c_int), ("kind", ctypes.c_int)]
+
+
+MAX_WGRAD_BATCH = 32
 
 
 class NativeLibraryError(RuntimeError):

@@ -343,7 +343,40 @@ def _in_bwd_stats(B, C, T, HW, part, like):
     return bst
 
 
+# Weight-gradient slice reductions queued inside `batched_wgrad_reduce()` run as ONE batched
+# pair of launches when the block exits (ebsdvae_wgrad_reduce_batch) instead of two launches
+# per layer; outside such a block they run immediately.  Results are bit-identical.
+_RQ = None
+
+
+@contextlib.contextmanager
+def batched_wgrad_reduce():
+    global _RQ
+    outer, q = _RQ, []
+    _RQ = q
+    try:
+        yield
+    finally:
+        _RQ = outer
+        _flush_reduces(q)
+
+
+def _flush_reduces(q):
+    for i in range(0, len(q), N.MAX_WGRAD_BATCH):
+        chunk = q[i:i + N.MAX_WGRAD_BATCH]
+        descs = (N.WgradReduceDesc * len(chunk))(*[
+            N.WgradReduceDesc(N.ptr(wp), N.ptr(bp), N.ptr(dw), N.ptr(db), S_, cin, cout, kind)
+            for wp, bp, S_, cin, cout, kind, dw, db in chunk])
+        nbytes = N.call("ebsdvae_wgrad_reduce_batch_work", ctypes.addressof(descs), len(chunk))
+        work = torch.empty(nbytes // 8, dtype=torch.float64, device=chunk[0][0].device)
+        N.call("ebsdvae_wgrad_reduce_batch", ctypes.addressof(descs), len(chunk), work.data_ptr(),
+               N.stream())
+
+
 def _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db):
+    if _RQ is not None:
+        _RQ.append((wpart, bpart, S_, cin, cout, kind, dw, db))
+        return
     nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
     work = torch.empty(nbytes // 8, dtype=torch.float64, device=wpart.device)
     N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db), cin, cout,
@@ -410,10 +443,7 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
     else:
         _launch("conv3x3_wgrad", conv_flops(B, H, W, cin, cout), N.call, "ebsdvae_conv3x3_wgrad",
                 *args, s, tag=tag)
-    nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
-    work = torch.empty(nbytes // 8, dtype=torch.float64, device=gy.device)
-    N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db),
-           cin, cout, kind, work.data_ptr(), s)
+    _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
 
 
 def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None):
@@ -488,7 +518,13 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True):
 
 
 def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=False, packs=None):
-    """g_enc: grad of the encoder output (B,s,s,C) NHWC.  Returns (grads dict, gx or None)."""
+    """g_enc: grad of the encoder output (B,s,s,C) NHWC.  Returns (grads dict, gx or None).
+    The layers' weight-gradient reductions run batched when it returns."""
+    with batched_wgrad_reduce():
+        return _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs)
+
+
+def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
     out = {}
     g_next, part = g_enc, None
     gx = None
@@ -594,7 +630,13 @@ def decoder_forward(plan: Plan, dec_in, params, packs=None):
 
 
 def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None, packs=None):
-    """g_xhat: (B,1,S,S).  Returns (grads dict, g_dec_in (B,s,s,C) NHWC)."""
+    """g_xhat: (B,1,S,S).  Returns (grads dict, g_dec_in (B,s,s,C) NHWC).  The layers'
+    weight-gradient reductions run batched when it returns."""
+    with batched_wgrad_reduce():
+        return _decoder_backward(plan, g_xhat, saved, params, grads, packs)
+
+
+def _decoder_backward(plan, g_xhat, saved, params, grads, packs):
     out = {}
     B = g_xhat.shape[0]
     S, p = plan.image_size, plan.inplanes

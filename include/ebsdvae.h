@@ -143,6 +143,21 @@ int ebsdvae_conv3x3_wgrad_split(const float* src, const float* src_stats, int sr
 int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
                          float* db, int cin, int cout, int kind, void* work,
                          ebsdvae_stream_t stream);
+/* Batched form: the slice reductions of n <= EBSDVAE_MAX_WGRAD_BATCH layers in two launches (the
+ * per-layer form costs two launches per layer).  Each layer's result is bit-identical to
+ * ebsdvae_wgrad_reduce.  descs live in HOST memory (passed to the kernels by value); work is
+ * device scratch of ebsdvae_wgrad_reduce_batch_work(descs, n) bytes. */
+#define EBSDVAE_MAX_WGRAD_BATCH 32
+typedef struct {
+  const float* wpart; /* device, [slices][tap][cout][cin] */
+  const float* bpart; /* device, [slices][cout] */
+  float* dw;          /* device, parameter layout of `kind` */
+  float* db;          /* device or NULL */
+  int slices, cin, cout, kind;
+} ebsdvae_wgrad_reduce_desc;
+size_t ebsdvae_wgrad_reduce_batch_work(const ebsdvae_wgrad_reduce_desc* descs, int n);
+int ebsdvae_wgrad_reduce_batch(const ebsdvae_wgrad_reduce_desc* descs, int n, void* work,
+                               ebsdvae_stream_t stream);
 
 /* ---- InstanceNorm2d + LeakyReLU (latice/model.py:96-97,105-106) -----------------------
  * combine conv-epilogue partials {mean,M2} (tiles per image, n elements each) into

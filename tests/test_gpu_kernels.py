@@ -408,6 +408,38 @@ def test_batched_weight_pack_matches_single_packs(cuda):
             assert pd.pieces == single.pieces and torch.equal(pd.t, single.t), L.name
 
 
+def test_batched_wgrad_reduce_matches_per_layer(cuda):
+    """ebsdvae_wgrad_reduce_batch (two launches for many layers) is bit-identical to the
+    per-layer ebsdvae_wgrad_reduce, for conv and convT layouts, with and without bias."""
+    rng = np.random.default_rng(23)
+    layers = [(300, 32, 32, E.KIND_CONV, True), (17, 64, 128, E.KIND_CONVT, True),
+              (64, 1, 32, E.KIND_CONV, True), (5, 32, 1, E.KIND_CONV, False)]
+    items, singles = [], []
+    for S_, cin, cout, kind, has_b in layers:
+        wp = dev(rng.standard_normal((S_, 9, cout, cin)))
+        bp = dev(rng.standard_normal((S_, cout)))
+        shape = (cout, cin, 3, 3) if kind == E.KIND_CONV else (cin, cout, 3, 3)
+        dw_b, dw_s = torch.empty(shape, device="cuda"), torch.empty(shape, device="cuda")
+        db_b = torch.empty(cout, device="cuda") if has_b else None
+        db_s = torch.empty(cout, device="cuda") if has_b else None
+        items.append((wp, bp, S_, cin, cout, kind, dw_b, db_b))
+        singles.append((wp, bp, S_, cin, cout, kind, dw_s, db_s))
+    with E.batched_wgrad_reduce():
+        for it in items:
+            E._reduce_slices(*it)
+    for it in singles:
+        E._reduce_slices(*it)
+    torch.cuda.synchronize()
+    for (wp, bp, S_, cin, cout, kind, dwb, dbb), (*_, dws, dbs) in zip(items, singles):
+        assert torch.equal(dwb, dws)
+        if dbb is not None:
+            assert torch.equal(dbb, dbs)
+        ref = host(wp).sum(0)   # [tap][co][ci]
+        ref = ref.transpose(1, 2, 0).reshape(cout, cin, 3, 3) if kind == E.KIND_CONV else \
+            ref.transpose(2, 1, 0)[:, :, ::-1].reshape(cin, cout, 3, 3)
+        assert np.abs(host(dwb) - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
+
+
 SPLIT_TOL = {"bf16x3": 1e-4, "bf16x6": 2e-5}   # ~2^-16.5 / ~2^-25 per product
 
 
