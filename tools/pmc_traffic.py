@@ -24,6 +24,7 @@ FAMILIES = [
     ("conv3x3_big_kernel", "conv3x3_fwd"),
     ("conv3x3_small_kernel", "conv3x3_fwd"),
     ("conv3x3_split_kernel", "conv3x3_fwd"),
+    ("conv3x3_pipe_kernel", "conv3x3_fwd"),
     ("ev::wgrad_kernel<", "conv3x3_wgrad"),
     ("wgrad_split_kernel", "conv3x3_wgrad"),
     ("pack_split", "pack_weight"),
