@@ -69,13 +69,17 @@ SIGNATURES = {
     "ebsdvae_vae_loss_fwd": [P, P, P, P, P, F, P, P, P, P, P, P, I, I, I, P],
     "ebsdvae_vae_loss_bwd": [P, P, P, P, P, F, P, P, P, P, F, P, P, P, P, P, I, I, I, P],
     "ebsdvae_adam": [P, P, P, P, P, P, I64, F, F, F, F, F, I, P],
+    "ebsdvae_l2_normalize_rows": [P, P, I64, I, P],
+    "ebsdvae_cosine_topk_work": [I64, I, I, I],
+    "ebsdvae_cosine_topk": [P, I64, P, I, I, I, P, P, P, P],
 }
 _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t,
             "ebsdvae_wgrad_reduce_batch_work": ctypes.c_size_t,
+            "ebsdvae_cosine_topk_work": ctypes.c_size_t,
             "ebsdvae_heads_wgrad_work": ctypes.c_size_t, "ebsdvae_pack_split_bytes": ctypes.c_size_t}
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
-           "ebsdvae_wgrad_reduce_batch_work",
+           "ebsdvae_wgrad_reduce_batch_work", "ebsdvae_cosine_topk_work",
            "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices"}

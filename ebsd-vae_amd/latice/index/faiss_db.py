@@ -1,0 +1,202 @@
+"""Drop-in for latice/index/faiss_db.py (FaissLatentVectorDatabase) on the MI355X path.
+
+The reference keeps L2-normalised latent vectors in a faiss-cpu 1.10 `IndexFlatIP`
+(exhaustive inner product = cosine similarity, faiss_db.py:126-139) and answers
+`query_similar` one query at a time (:216-256).  Here the normalised dictionary lives in HBM
+as an N x D fp32 tensor and queries run as batched HIP launches (csrc/search.hip):
+
+    ebsdvae_l2_normalize_rows   faiss_db.py:107-111 (norm 0 -> 1)
+    ebsdvae_cosine_topk         IndexFlatIP.search: k best by score, ties to the lower row
+
+There is no CPU or faiss fallback: the dictionary must sit on a ROCm device.  Persistence
+is one .npz with the normalised `latents` and the `orientations` (the reference pickles a
+serialised faiss index into the same file, faiss_db.py:426-445; that format needs faiss).
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from .. import _native as N
+
+logger = logging.getLogger(__name__)
+
+MAX_K = 64
+
+
+@dataclass
+class FaissLatentVectorDatabaseConfig:
+    """faiss_db.py:35-46 (+ the device the dictionary lives on)."""
+    npz_path: str = "faiss_index.npz"
+    dimension: int = 16
+    device: str = "cuda"
+
+
+@dataclass
+class OrientationResult:
+    """faiss_db.py:49-89 (identical fields)."""
+    query_vector: np.ndarray
+    best_orientation: np.ndarray
+    candidate_orientations: np.ndarray
+    distances: np.ndarray
+    mean_orientation: np.ndarray | None = None
+    success: bool = True
+    similar_indices: np.ndarray | None = None
+
+    def get_top_n_orientations(self, n: int = 5) -> np.ndarray:
+        """faiss_db.py:72-89 (sorts by ascending distance, as the reference does)."""
+        if self.distances is None or len(self.distances) == 0:
+            return self.candidate_orientations[: min(n, len(self.candidate_orientations))]
+        order = np.argsort(self.distances)
+        return self.candidate_orientations[order[: min(n, len(order))]]
+
+
+def _as_device_f32(x, device) -> torch.Tensor:
+    t = torch.as_tensor(x)
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+def l2_normalize(x: torch.Tensor) -> torch.Tensor:
+    """Row-wise v / ||v|| on the device (faiss_db.py:107-111)."""
+    if not x.is_cuda:
+        raise RuntimeError("l2_normalize needs a ROCm device tensor (no CPU fallback)")
+    x = x.to(torch.float32).contiguous()
+    y = torch.empty_like(x)
+    N.call("ebsdvae_l2_normalize_rows", x.data_ptr(), y.data_ptr(), x.shape[0], x.shape[1],
+           N.stream(x.device))
+    return y
+
+
+def cosine_topk(db: torch.Tensor, queries: torch.Tensor, k: int):
+    """Exact top-k of <q, db_i> over normalised rows; (scores (Q,k) fp32, idx (Q,k) int64),
+    best first, ties to the lower row index."""
+    if not (db.is_cuda and queries.is_cuda):
+        raise RuntimeError("cosine_topk needs ROCm device tensors (no CPU fallback)")
+    n, d = db.shape
+    q = queries.reshape(-1, d).contiguous()
+    Q = q.shape[0]
+    scores = torch.empty(Q, k, dtype=torch.float32, device=db.device)
+    idx = torch.empty(Q, k, dtype=torch.int64, device=db.device)
+    nbytes = N.call("ebsdvae_cosine_topk_work", n, Q, d, k)
+    work = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=db.device)
+    N.call("ebsdvae_cosine_topk", db.data_ptr(), n, q.data_ptr(), Q, d, k, scores.data_ptr(),
+           idx.data_ptr(), work.data_ptr(), N.stream(db.device))
+    return scores, idx
+
+
+class FaissLatentVectorDatabase:
+    """faiss_db.py:92-496 with an HBM-resident dictionary and HIP search."""
+
+    def __init__(self, config: FaissLatentVectorDatabaseConfig | None = None) -> None:
+        self.config = config if config is not None else FaissLatentVectorDatabaseConfig()
+        self.dimension = self.config.dimension
+        self.npz_path = Path(self.config.npz_path)
+        self.device = torch.device(self.config.device)
+        self._db = torch.empty(0, self.dimension, dtype=torch.float32, device=self.device)
+        self._orientations = np.empty((0, 3), dtype=np.float64)
+        if self.npz_path.exists():
+            self.load()
+        else:
+            logger.info(f"No existing index found at {self.npz_path}. Creating a new one.")
+
+    # ------------------------------------------------------------------ population
+    def _validate_vectors(self, latent_vectors, orientations) -> None:
+        """faiss_db.py:141-158."""
+        if len(latent_vectors) != len(orientations):
+            raise ValueError("Number of latent vectors and orientations must match")
+        if latent_vectors.shape[1] != self.dimension:
+            raise ValueError(f"Expected latent vectors of dimension {self.dimension}, "
+                             f"got {latent_vectors.shape[1]}")
+        if orientations.shape[1] != 3:
+            raise ValueError(f"Expected orientations of shape (n, 3), got {orientations.shape}")
+
+    def add_vectors(self, latent_vectors, orientations) -> None:
+        """faiss_db.py:160-189: cast to fp32, L2-normalise, append (numpy or device tensors;
+        device tensors from `encode_mu` never leave HBM)."""
+        orientations = np.asarray(orientations, dtype=np.float64)
+        if orientations.ndim == 1:
+            orientations = orientations.reshape(-1, 3)
+        lv = _as_device_f32(latent_vectors, self.device)
+        if lv.ndim != 2:
+            raise ValueError(f"latent vectors must be 2-D, got shape {tuple(lv.shape)}")
+        lv = l2_normalize(lv) if lv.shape[0] else lv
+        self._validate_vectors(lv, orientations)
+        self._db = torch.cat([self._db, lv], 0)
+        self._orientations = np.concatenate([self._orientations, orientations], 0)
+        logger.info(f"Added {lv.shape[0]} vectors. Index total: {self.get_count()}")
+
+    def create_from_files(self, latent_file_path, angles_file_path) -> None:
+        """faiss_db.py:191-214."""
+        lv = np.load(Path(latent_file_path)).astype(np.float32)
+        ori = np.load(Path(angles_file_path))
+        self.add_vectors(lv, ori)
+        self.save()
+
+    # ------------------------------------------------------------------ queries
+    def query_similar_batch(self, query_vectors, n_results: int = 20):
+        """Batched query_similar: (distances (Q,k) fp32, indices (Q,k) int64) as numpy, the
+        GPU search running once for all Q queries."""
+        count = self.get_count()
+        if count == 0:
+            logger.warning("Querying an empty index.")
+            return np.empty((0, 0), np.float32), np.empty((0, 0), np.int64)
+        if count < n_results:
+            logger.warning(f"Requested {n_results} results, but index only contains {count} "
+                           "vectors. Returning all.")
+            n_results = count
+        if n_results > MAX_K:
+            raise ValueError(f"n_results={n_results} > {MAX_K} (GPU top-k limit)")
+        q = _as_device_f32(query_vectors, self.device)
+        if q.ndim == 1:
+            q = q.reshape(1, -1)
+        if q.shape[1] != self.dimension:
+            raise ValueError(f"Expected query vector of dimension {self.dimension}, got {q.shape[1]}")
+        s, i = cosine_topk(self._db, l2_normalize(q), n_results)
+        return s.cpu().numpy(), i.cpu().numpy()
+
+    def query_similar(self, query_vector, n_results: int = 20):
+        """faiss_db.py:216-256: distances (cosine similarity) and indices of one query."""
+        d, i = self.query_similar_batch(query_vector, n_results)
+        if d.size == 0:
+            return np.array([]), np.array([])
+        return d[0], i[0]
+
+    # ------------------------------------------------------------------ bookkeeping
+    def get_count(self) -> int:
+        return int(self._db.shape[0])
+
+    @property
+    def orientations(self) -> np.ndarray:
+        return self._orientations
+
+    def save(self) -> None:
+        """One .npz: normalised latents + orientations (faiss_db.py:426-445 stores a faiss
+        blob instead)."""
+        np.savez_compressed(str(self.npz_path.with_suffix(".npz")),
+                            latents=self._db.cpu().numpy(), orientations=self._orientations)
+        logger.info(f"Saved index and metadata to {self.npz_path.with_suffix('.npz')}")
+
+    def load(self) -> None:
+        """faiss_db.py:447-466 for the .npz this class writes (no pickles)."""
+        path = self.npz_path.with_suffix(".npz")
+        if not path.exists():
+            raise FileNotFoundError("NPZ file missing.")
+        with np.load(str(path), allow_pickle=False) as data:
+            if "latents" not in data:
+                raise ValueError(f"{path} has no 'latents' array (a faiss-serialised index "
+                                 "needs faiss to read; re-create it with add_vectors)")
+            lv = data["latents"].astype(np.float32)
+            self._orientations = data["orientations"].astype(np.float64).reshape(-1, 3)
+        self.dimension = lv.shape[1]
+        self._db = torch.from_numpy(lv).to(self.device)
+
+    def delete_persistence(self) -> None:
+        """faiss_db.py:468-496."""
+        if self.npz_path.exists():
+            self.npz_path.unlink()
+            self._db = torch.empty(0, self.dimension, dtype=torch.float32, device=self.device)
+            self._orientations = np.empty((0, 3), dtype=np.float64)

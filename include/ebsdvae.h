@@ -278,6 +278,20 @@ int ebsdvae_adam(float* p, const float* g, float* m, float* v, float* vmax, floa
                  int64_t n, float lr, float beta1, float beta2, float eps,
                  float weight_decay, int amsgrad, ebsdvae_stream_t stream);
 
+/* ---- latent dictionary search ---------------------------
+ * GPU form of latice/index/faiss_db.py's IndexFlatIP cosine search: rows are L2-normalised
+ * (norm 0 -> 1, faiss_db.py:107-111) and queried exhaustively by inner product.
+ * ebsdvae_cosine_topk writes, per query q, the k (1..64, <= N) best dictionary rows ordered
+ * by (score desc, row index asc): out_scores[q][k] (fp32), out_idx[q][k] (int64).  d is 16,
+ * 32 or 64; db is N x d row-major, queries Q x d, both already normalised.  work: device
+ * scratch of ebsdvae_cosine_topk_work(N, Q, d, k) bytes. */
+int ebsdvae_l2_normalize_rows(const float* x, float* y, long long n, int d,
+                              ebsdvae_stream_t stream);
+size_t ebsdvae_cosine_topk_work(long long N, int Q, int d, int k);
+int ebsdvae_cosine_topk(const float* db, long long N, const float* queries, int Q, int d, int k,
+                        float* out_scores, long long* out_idx, void* work,
+                        ebsdvae_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
