@@ -7,6 +7,7 @@ as an N x D fp32 tensor and queries run as batched HIP launches (csrc/search.hip
 
     ebsdvae_l2_normalize_rows   faiss_db.py:107-111 (norm 0 -> 1)
     ebsdvae_cosine_topk         IndexFlatIP.search: k best by score, ties to the lower row
+    ebsdvae_orient_consensus    find_best_orientation (:258-398), all queries in one launch
 
 There is no CPU or faiss fallback: the dictionary must sit on a ROCm device.  Persistence
 is one .npz with the normalised `latents` and the `orientations` (the reference pickles a
@@ -98,6 +99,7 @@ class FaissLatentVectorDatabase:
         self.device = torch.device(self.config.device)
         self._db = torch.empty(0, self.dimension, dtype=torch.float32, device=self.device)
         self._orientations = np.empty((0, 3), dtype=np.float64)
+        self._ori_dev = torch.empty(0, 3, dtype=torch.float64, device=self.device)
         if self.npz_path.exists():
             self.load()
         else:
@@ -127,6 +129,7 @@ class FaissLatentVectorDatabase:
         self._validate_vectors(lv, orientations)
         self._db = torch.cat([self._db, lv], 0)
         self._orientations = np.concatenate([self._orientations, orientations], 0)
+        self._ori_dev = torch.cat([self._ori_dev, torch.from_numpy(orientations).to(self.device)], 0)
         logger.info(f"Added {lv.shape[0]} vectors. Index total: {self.get_count()}")
 
     def create_from_files(self, latent_file_path, angles_file_path) -> None:
@@ -165,6 +168,68 @@ class FaissLatentVectorDatabase:
             return np.array([]), np.array([])
         return d[0], i[0]
 
+    # ------------------------------------------------------------------ orientation consensus
+    def find_best_orientations_batch(self, query_vectors, batch_size: int = 32, top_n: int = 20,
+                                     orientation_threshold: float = 1.0,
+                                     min_required_matches: int = 18,
+                                     max_iterations: int = 3) -> list[OrientationResult]:
+        """faiss_db.py:400-438 (which loops find_best_orientation per vector): here ONE
+        cosine top-k launch and ONE consensus launch serve every query (batch_size only
+        bounds the launch size)."""
+        qv = np.asarray(query_vectors.detach().cpu() if torch.is_tensor(query_vectors) else query_vectors)
+        qv = qv.reshape(-1, self.dimension)
+        count = self.get_count()
+        if count == 0:
+            logger.warning("No similar vectors found for query.")
+            return [OrientationResult(query_vector=v.squeeze(), best_orientation=np.full(3, np.nan),
+                                      candidate_orientations=np.array([]), distances=np.array([]),
+                                      mean_orientation=None, success=False, similar_indices=None)
+                    for v in qv]
+        k = min(top_n, count)
+        if k > MAX_K:
+            raise ValueError(f"top_n={top_n} > {MAX_K} (GPU top-k limit)")
+        out = []
+        step = max(int(batch_size), 1) * 1024   # queries per launch pair
+        for s0 in range(0, len(qv), step):
+            q = _as_device_f32(qv[s0:s0 + step], self.device)
+            scores, idx = cosine_topk(self._db, l2_normalize(q), k)
+            Q = q.shape[0]
+            best = torch.empty(Q, 3, dtype=torch.float64, device=self.device)
+            mean = torch.empty(Q, 3, dtype=torch.float64, device=self.device)
+            ok = torch.empty(Q, dtype=torch.int32, device=self.device)
+            mask = torch.empty(Q, dtype=torch.int64, device=self.device)
+            N.call("ebsdvae_orient_consensus", self._ori_dev.data_ptr(), idx.data_ptr(), Q, k,
+                   float(orientation_threshold), int(min_required_matches), int(max_iterations),
+                   best.data_ptr(), mean.data_ptr(), ok.data_ptr(), mask.data_ptr(),
+                   N.stream(self.device))
+            scores, idx = scores.cpu().numpy(), idx.cpu().numpy()
+            best, mean = best.cpu().numpy(), mean.cpu().numpy()
+            ok, mask = ok.cpu().numpy(), mask.cpu().numpy().view(np.uint64)
+            iters = min(max_iterations, k)
+            for j in range(Q):
+                bits = int(mask[j])
+                sim = (np.array([b for b in range(k) if (bits >> b) & 1], dtype=np.int64)
+                       if iters > 0 else None)
+                succ = bool(ok[j])
+                if not succ:
+                    logger.warning("Failed to find consensus orientation after "
+                                   f"{iters} iterations. Best guess is the closest match: {best[j]}")
+                out.append(OrientationResult(
+                    query_vector=qv[s0 + j].squeeze().astype(np.float64),
+                    best_orientation=best[j], mean_orientation=mean[j] if succ else None,
+                    candidate_orientations=self._orientations[idx[j]], distances=scores[j],
+                    success=succ, similar_indices=sim))
+        return out
+
+    def find_best_orientation(self, query_vector, top_n: int = 20,
+                              orientation_threshold: float = 1.0, min_required_matches: int = 18,
+                              max_iterations: int = 3) -> OrientationResult:
+        """faiss_db.py:258-372 for one query (runs the batched kernels with Q = 1)."""
+        return self.find_best_orientations_batch(
+            np.asarray(query_vector).reshape(1, -1), top_n=top_n,
+            orientation_threshold=orientation_threshold,
+            min_required_matches=min_required_matches, max_iterations=max_iterations)[0]
+
     # ------------------------------------------------------------------ bookkeeping
     def get_count(self) -> int:
         return int(self._db.shape[0])
@@ -193,6 +258,7 @@ class FaissLatentVectorDatabase:
             self._orientations = data["orientations"].astype(np.float64).reshape(-1, 3)
         self.dimension = lv.shape[1]
         self._db = torch.from_numpy(lv).to(self.device)
+        self._ori_dev = torch.from_numpy(self._orientations).to(self.device)
 
     def delete_persistence(self) -> None:
         """faiss_db.py:468-496."""
@@ -200,3 +266,4 @@ class FaissLatentVectorDatabase:
             self.npz_path.unlink()
             self._db = torch.empty(0, self.dimension, dtype=torch.float32, device=self.device)
             self._orientations = np.empty((0, 3), dtype=np.float64)
+            self._ori_dev = torch.empty(0, 3, dtype=torch.float64, device=self.device)

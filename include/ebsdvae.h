@@ -292,6 +292,17 @@ int ebsdvae_cosine_topk(const float* db, long long N, const float* queries, int 
                         float* out_scores, long long* out_idx, void* work,
                         ebsdvae_stream_t stream);
 
+/* ---- orientation consensus ------------------------------
+ * Batched latice/index/faiss_db.py:258-398 find_best_orientation (== chroma_db.py:261-375):
+ * query q's candidates are orientations[cand_idx[q][0..n-1]] (ZXZ Euler degrees, float64,
+ * top-n match order; n <= 64).  Writes best[q][3] (the symmetry-resolved mean on success,
+ * else candidate 0), mean[q][3] (NaN when no consensus), success[q] (0/1) and
+ * similar_mask[q] (bit j = candidate j within threshold_deg of the last reference tried). */
+int ebsdvae_orient_consensus(const double* orientations, const long long* cand_idx, int Q, int n,
+                             double threshold_deg, int min_matches, int max_iterations,
+                             double* best, double* mean, int* success,
+                             unsigned long long* similar_mask, ebsdvae_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -88,3 +88,58 @@ def test_database_api(cuda, tmp_path):
     assert np.array_equal(i2, db.query_similar(q, n_results=20)[1])
     db2.delete_persistence()
     assert db2.get_count() == 0
+
+
+def _cluster_db(rng, n_clusters=40, per=24, noise_deg=0.3, dim=16):
+    """Latents clustered per orientation; orientations noisy around cluster centres, some
+    copies hidden behind random cubic symmetry operators."""
+    from scipy.spatial.transform import Rotation as R
+    sym = R.from_quat(IO.CUBIC_SYMMETRY)
+    lat, ori = [], []
+    for c in range(n_clusters):
+        centre = R.random(random_state=int(rng.integers(1 << 30)))
+        z = rng.standard_normal(dim)
+        for j in range(per):
+            rot = R.from_rotvec(np.radians(noise_deg) * rng.standard_normal(3)) * centre
+            if j % 7 == 3:
+                rot = sym[int(rng.integers(24))] * rot
+            ori.append(rot.as_euler("zxz", degrees=True))
+            lat.append(z + 0.05 * rng.standard_normal(dim))
+    return np.array(lat, np.float32), np.array(ori)
+
+
+@pytest.mark.parametrize("thr,minm,maxit", [(1.0, 18, 3), (2.0, 12, 3), (1.0, 15, 2), (5.0, 1, 1), (0.5, 21, 3)])
+def test_orientation_consensus_matches_oracle(cuda, thr, minm, maxit):
+    rng = np.random.default_rng(int(thr * 10) + minm + maxit)
+    lat, ori = _cluster_db(rng)
+    db = F.FaissLatentVectorDatabase(F.FaissLatentVectorDatabaseConfig(npz_path="/nonexistent/x.npz"))
+    db.add_vectors(lat, ori)
+    queries = lat[::9] + 0.02 * rng.standard_normal((len(lat[::9]), 16)).astype(np.float32)
+    res = db.find_best_orientations_batch(queries, top_n=20, orientation_threshold=thr,
+                                          min_required_matches=minm, max_iterations=maxit)
+    n_ok = 0
+    for r in res:
+        best, mean, ok, sim = IO.find_best_orientation(r.candidate_orientations, thr, minm, maxit)
+        assert r.success == ok
+        assert np.array_equal(r.similar_indices, sim)
+        if ok:
+            n_ok += 1
+            # same rotation; Euler angles compared modulo 360 (wrap at +-180)
+            d = (np.asarray(r.best_orientation) - best + 180.0) % 360.0 - 180.0
+            assert np.abs(d).max() < 1e-6, (r.best_orientation, best)
+            assert r.mean_orientation is not None
+        else:
+            assert r.mean_orientation is None and np.array_equal(r.best_orientation, best)
+    assert n_ok > 0 or minm > 20   # more required matches than candidates: never
+
+
+def test_single_query_api_and_empty_index(cuda):
+    rng = np.random.default_rng(11)
+    lat, ori = _cluster_db(rng, n_clusters=5)
+    db = F.FaissLatentVectorDatabase(F.FaissLatentVectorDatabaseConfig(npz_path="/nonexistent/y.npz"))
+    r = db.find_best_orientation(lat[0])
+    assert not r.success and np.isnan(r.best_orientation).all()
+    db.add_vectors(lat, ori)
+    r = db.find_best_orientation(lat[0], top_n=20, orientation_threshold=2.0, min_required_matches=10)
+    best, mean, ok, sim = IO.find_best_orientation(r.candidate_orientations, 2.0, 10, 3)
+    assert r.success == ok and r.candidate_orientations.shape == (20, 3) and r.distances.shape == (20,)
