@@ -73,6 +73,7 @@ SIGNATURES = {
     "ebsdvae_cosine_topk_work": [I64, I, I, I],
     "ebsdvae_cosine_topk": [P, I64, P, I, I, I, P, P, P, P],
     "ebsdvae_orient_consensus": [P, P, I, I, ctypes.c_double, I, I, P, P, P, P, P],
+    "ebsdvae_ingest_patterns": [P, I, I, I, I, I, I, P, P],
 }
 _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t,
             "ebsdvae_wgrad_reduce_batch_work": ctypes.c_size_t,

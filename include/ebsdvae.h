@@ -303,6 +303,14 @@ int ebsdvae_orient_consensus(const double* orientations, const long long* cand_i
                              double* best, double* mean, int* success,
                              unsigned long long* similar_mask, ebsdvae_stream_t stream);
 
+/* ---- pattern ingest -------------------------------------
+ * Batched DPdataset.__getitem__ transform (latice/data_module.py:17-33,125-133): raw
+ * (B, H0, W0) patterns (src_dtype 0 = float64, 1 = float32) -> uint8(x * 255) -> centre
+ * crop / zero-pad to (out_h, out_w) as torchvision's CenterCrop -> float32 / 255, written as
+ * dst (B, 1, out_h, out_w).  Values outside [0, 1] are clamped before the uint8 cast. */
+int ebsdvae_ingest_patterns(const void* src, int src_dtype, int B, int H0, int W0, int out_h,
+                            int out_w, float* dst, ebsdvae_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,3 +65,39 @@ def find_best_orientation(candidates_euler, orientation_threshold=1.0, min_requi
             success, best = True, mean
             break
     return best, mean, success, similar
+
+
+# ----------------------------------------------------------------------------- ingest
+def _py_round_half_even(x: float) -> int:
+    return int(round(x))   # Python's round: ties to even, as torchvision's center_crop uses
+
+
+def ingest_patterns(raw: np.ndarray, image_size=(128, 128)) -> np.ndarray:
+    """latice/data_module.py:17-33,125-133: float64 cast, torchvision ToPILImage on a float
+    ndarray ((x * 255).astype(uint8), clamped here to [0, 255] -- numpy's out-of-range cast is
+    platform-defined), Grayscale (identity on "L"), CenterCrop (zero pad ((c-s)//2,
+    (c-s+1)//2) when too small, else offset round((s-c)/2)), ToTensor (/255 in float32).
+    torchvision 0.21 is not installed here: this restates its published algorithm (parity with
+    torchvision itself unpinned)."""
+    x = np.asarray(raw, dtype=np.float64)
+    if x.ndim == 2:
+        x = x[None]
+    B, H0, W0 = x.shape
+    u8 = np.clip(np.nan_to_num(x * 255.0, nan=0.0), 0, 255).astype(np.uint8)
+    h, w = image_size
+    out = np.zeros((B, 1, h, w), np.float32)
+
+    def axis(size, crop):
+        if crop > size:
+            return -((crop - size) // 2)
+        return _py_round_half_even((size - crop) / 2.0)
+
+    top, left = axis(H0, h), axis(W0, w)
+    for y in range(h):
+        sy = y + top
+        if not 0 <= sy < H0:
+            continue
+        xs = np.arange(w) + left
+        ok = (xs >= 0) & (xs < W0)
+        out[:, 0, y, ok] = u8[:, sy, xs[ok]].astype(np.float32) / np.float32(255.0)
+    return out
