@@ -100,38 +100,69 @@ def cpu_baseline(plan, seconds: float, batch: int):
 
 
 def encoder_latents(model, plan, args, dev, world):
-    """BASELINE c4: encoder-only inference (encoder + mu head, the build_dictionary path) at
-    batch 1024 per GPU on synthetic patterns resident in HBM; no collective (every rank
-    encodes its own shard)."""
+    """BASELINE c4: DiffractionPatternIndexer.build_dictionary (latice/index/dp_indexer.py:
+    92-111, 254-297) end to end on the device, at batch 1024 per GPU: raw float64 patterns
+    (synthetic, already in HBM) -> the DPdataset transform (ebsdvae_ingest_patterns) ->
+    encoder + mu head (encode_latents) -> L2-normalised rows appended to the HBM dictionary
+    (latice.index.faiss_db).  c4_batches (default 1024 = 1,048,576 patterns) are split over
+    the ranks; no collective.  Then one batched query of 4096 latents against the dictionary:
+    cosine top-20 + orientation consensus (faiss_db.find_best_orientations_batch)."""
     from latice import engine as E
-    from latice.seeding import synthetic_patterns
-    B = 1024
+    from latice.data_module import ingest_patterns
+    from latice.index.faiss_db import FaissLatentVectorDatabase, FaissLatentVectorDatabaseConfig
+    import logging
+    logging.getLogger("latice.index.faiss_db").setLevel(logging.ERROR)   # random angles never agree
+    B, S = 1024, args.image_size
+    H0 = S + 12   # raw patterns a little larger than the crop, as in the reference pipeline
+    nb = max(1, args.c4_batches // world)
     params = dict(model.named_parameters())
-    x = torch.from_numpy(synthetic_patterns(7, B, args.image_size)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(7 + dist.get_rank() if world > 1 else 7)
+    raw = torch.rand(B, H0, H0, dtype=torch.float64, device=dev, generator=gen)
+    angles = np.random.default_rng(11).uniform(0.0, 360.0, (nb * B, 3))
+    x = torch.empty(B, 1, S, S, dtype=torch.float32, device=dev)
     packs = E.PackSet(plan, params).refresh()
+    db = FaissLatentVectorDatabase(FaissLatentVectorDatabaseConfig(
+        npz_path="/nonexistent/c4_dictionary.npz", dimension=plan.latent_dim, device=str(dev)))
+    db.reserve(nb * B)
     with torch.no_grad():
         for _ in range(2):
-            E.encode_latents(plan, x, params, packs)
+            E.encode_latents(plan, ingest_patterns(raw, (S, S), out=x), params, packs)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.c4_batches):
-            mu = E.encode_latents(plan, x, params, packs)
+        for i in range(nb):
+            mu = E.encode_latents(plan, ingest_patterns(raw, (S, S), out=x), params, packs)
+            db.add_vectors(mu, angles[i * B:(i + 1) * B])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        finite = bool(torch.isfinite(mu).all())
+        # query leg: 4096 perturbed latents, top-20 + consensus over the whole dictionary
+        q = (mu.repeat(4, 1) + 0.01 * torch.randn(4 * B, plan.latent_dim, device=dev, generator=gen))
+        db.find_best_orientations_batch(q[:64], top_n=20)   # warm-up
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        res = db.find_best_orientations_batch(q, top_n=20)
+        torch.cuda.synchronize()
+        qel = time.perf_counter() - t1
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el, qel], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t)
-    n = world * B * args.c4_batches
+        el, qel = float(t[0]), float(t[1])
+    n = world * B * nb
     enc_flops = sum(2.0 * L.H * L.H * L.cin * L.cout * 9 for L in plan.enc) + 2 * plan.feat * plan.latent_dim
-    return {"metric": "encoder latents/sec (c4: encoder + mu head, batch 1024/GPU)",
+    return {"metric": "encoder latents/sec (c4: build_dictionary = ingest + encoder + mu head + "
+                      "dictionary add, batch 1024/GPU)",
             "value": round(n / el, 1), "unit": "latents/s", "latents": n,
-            "ms_per_batch": round(el / args.c4_batches * 1e3, 3),
-            "tflops": round(enc_flops * n / el / 1e12, 2), "finite": bool(torch.isfinite(mu).all())}
+            "ms_per_batch": round(el / nb * 1e3, 3),
+            "tflops": round(enc_flops * n / el / 1e12, 2), "finite": finite,
+            "query": {"metric": "queries/sec (cosine top-20 over the dictionary + orientation "
+                                "consensus, one batch per GPU)",
+                      "value": round(world * len(res) / qel, 1), "unit": "queries/s",
+                      "queries": world * len(res), "dictionary_rows_per_gpu": db.get_count(),
+                      "ms": round(qel * 1e3, 3)}}
 
 
 def main():
@@ -148,7 +179,7 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
     ap.add_argument("--precision", default=None, choices=["fp32", "bf16x6", "bf16x3"],
                     help="conv arithmetic (default: the engine default, bf16x6)")
-    ap.add_argument("--c4-batches", type=int, default=64,
+    ap.add_argument("--c4-batches", type=int, default=1024,
                     help="encoder-only inference batches of 1024 for the c4 latents/s field (0: skip)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "

@@ -151,8 +151,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(
       const int img = px / T::IPX, rem = px % T::IPX;
       const int r = rem / TW, c = rem % TW;
       const int gb = b0 + img;
+#ifdef EV_WG_NOLOAD   // timing experiment only (wrong results)
+      rg[k] = make_float4((float)r, (float)c, 1.f, 0.f);
+#else
       if (T::NI == 1 || gb < B)
         rg[k] = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + qg * 4);
+#endif
     }
 #pragma unroll
     for (int k = 0; k < KH; ++k) {
@@ -162,7 +166,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(
       const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
       if (pix < T::HALO && gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
         const int sh = UPS ? (gh >> 1) : gh, sw = UPS ? (gw >> 1) : gw;
+#ifdef EV_WG_NOLOAD
+        rh[k] = make_float4((float)sh, (float)sw, 1.f, 0.f);
+#else
         rh[k] = ld4(src + (((size_t)gb * Hs + sh) * Ws + sw) * Cin + ci0 + qh * 4);
+#endif
       }
     }
     if (NORM && T::NI == 1) load_stats(b0);
@@ -399,8 +407,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
       const int img = px / T::IPX, rem = px % T::IPX;
       const int r = rem / TW, c = rem % TW;
       const int gb = b0 + img;
+#ifdef EV_WG_NOLOAD   // timing experiment only (wrong results)
+      rg[k] = make_float4((float)r, (float)c, 1.f, 0.f);
+#else
       if (T::NI == 1 || gb < B)
         rg[k] = ld4(gy + (((size_t)gb * H + y0 + r) * W + x0 + c) * Cout + co0 + qg * 4);
+#endif
     }
 #pragma unroll
     for (int k = 0; k < KH; ++k) {
@@ -410,7 +422,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
       const int gh = y0 + hh - 1, gw = x0 + ww - 1, gb = b0 + img;
       if (pix < T::HALO && gb < B && gh >= 0 && gh < H && gw >= 0 && gw < W) {
         const int sh = UPS ? (gh >> 1) : gh, sw = UPS ? (gw >> 1) : gw;
+#ifdef EV_WG_NOLOAD
+        rh[k] = make_float4((float)sh, (float)sw, 1.f, 0.f);
+#else
         rh[k] = ld4(src + (((size_t)gb * Hs + sh) * Ws + sw) * Cin + ci0 + qh * 4);
+#endif
       }
     }
     if (NORM && T::NI == 1) load_stats(b0);
@@ -486,6 +502,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
         for (int i = 0; i < NP; ++i)
           b[i] = tr_frag(aimg + i * ACT_PIECE + (hp0 + toff) * WGS_ASB + bcol,
                          aimg + i * ACT_PIECE + (hp1 + toff) * WGS_ASB + bcol);
+#ifdef EV_WG_NOMFMA   // timing experiment only (wrong results)
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int i = 0; i < NP; ++i) acc[f][tap][i & 3] += (float)a[i][f][0] * (float)b[i][1];
+        if (false)
+#endif
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           f32x4 c = acc[f][tap];

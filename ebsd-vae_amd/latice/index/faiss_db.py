@@ -97,13 +97,54 @@ class FaissLatentVectorDatabase:
         self.dimension = self.config.dimension
         self.npz_path = Path(self.config.npz_path)
         self.device = torch.device(self.config.device)
-        self._db = torch.empty(0, self.dimension, dtype=torch.float32, device=self.device)
-        self._orientations = np.empty((0, 3), dtype=np.float64)
-        self._ori_dev = torch.empty(0, 3, dtype=torch.float64, device=self.device)
+        self._reset()
         if self.npz_path.exists():
             self.load()
         else:
             logger.info(f"No existing index found at {self.npz_path}. Creating a new one.")
+
+    # ------------------------------------------------------------------ storage
+    # Capacity-backed (amortised doubling), so appending batch after batch -- the
+    # build_dictionary pattern -- costs O(N) copies overall, not O(N^2).
+    def _reset(self, capacity: int = 0) -> None:
+        self._n = 0
+        self._cap_db = torch.empty(capacity, self.dimension, dtype=torch.float32, device=self.device)
+        self._cap_ori = np.empty((capacity, 3), dtype=np.float64)
+        self._cap_ori_dev = torch.empty(capacity, 3, dtype=torch.float64, device=self.device)
+
+    def reserve(self, capacity: int) -> None:
+        """Pre-size the dictionary for `capacity` rows (optional)."""
+        if capacity <= self._cap_db.shape[0]:
+            return
+        db, ori, ord_ = self._cap_db, self._cap_ori, self._cap_ori_dev
+        n = self._n
+        self._cap_db = torch.empty(capacity, self.dimension, dtype=torch.float32, device=self.device)
+        self._cap_ori = np.empty((capacity, 3), dtype=np.float64)
+        self._cap_ori_dev = torch.empty(capacity, 3, dtype=torch.float64, device=self.device)
+        self._cap_db[:n].copy_(db[:n])
+        self._cap_ori[:n] = ori[:n]
+        self._cap_ori_dev[:n].copy_(ord_[:n])
+
+    @property
+    def _db(self) -> torch.Tensor:
+        return self._cap_db[: self._n]
+
+    @property
+    def _orientations(self) -> np.ndarray:
+        return self._cap_ori[: self._n]
+
+    @property
+    def _ori_dev(self) -> torch.Tensor:
+        return self._cap_ori_dev[: self._n]
+
+    def _append(self, lv: torch.Tensor, ori: np.ndarray, ori_dev: torch.Tensor | None = None) -> None:
+        n, m = self._n, lv.shape[0]
+        if n + m > self._cap_db.shape[0]:
+            self.reserve(max(n + m, 2 * self._cap_db.shape[0], 1024))
+        self._cap_db[n:n + m].copy_(lv)
+        self._cap_ori[n:n + m] = ori
+        self._cap_ori_dev[n:n + m].copy_(ori_dev if ori_dev is not None else torch.from_numpy(ori))
+        self._n = n + m
 
     # ------------------------------------------------------------------ population
     def _validate_vectors(self, latent_vectors, orientations) -> None:
@@ -127,9 +168,7 @@ class FaissLatentVectorDatabase:
             raise ValueError(f"latent vectors must be 2-D, got shape {tuple(lv.shape)}")
         lv = l2_normalize(lv) if lv.shape[0] else lv
         self._validate_vectors(lv, orientations)
-        self._db = torch.cat([self._db, lv], 0)
-        self._orientations = np.concatenate([self._orientations, orientations], 0)
-        self._ori_dev = torch.cat([self._ori_dev, torch.from_numpy(orientations).to(self.device)], 0)
+        self._append(lv, orientations)
         logger.info(f"Added {lv.shape[0]} vectors. Index total: {self.get_count()}")
 
     def create_from_files(self, latent_file_path, angles_file_path) -> None:
@@ -206,18 +245,20 @@ class FaissLatentVectorDatabase:
             best, mean = best.cpu().numpy(), mean.cpu().numpy()
             ok, mask = ok.cpu().numpy(), mask.cpu().numpy().view(np.uint64)
             iters = min(max_iterations, k)
+            bits = ((mask[:, None] >> np.arange(k, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+            cands = self._orientations[idx]                   # (Q, k, 3)
+            lanes = np.arange(k, dtype=np.int64)
+            n_fail = int(Q - ok.sum())
+            if n_fail:
+                logger.warning(f"Failed to find consensus orientation for {n_fail} of {Q} queries "
+                               f"after {iters} iterations; their best guess is the closest match")
             for j in range(Q):
-                bits = int(mask[j])
-                sim = (np.array([b for b in range(k) if (bits >> b) & 1], dtype=np.int64)
-                       if iters > 0 else None)
+                sim = lanes[bits[j]] if iters > 0 else None
                 succ = bool(ok[j])
-                if not succ:
-                    logger.warning("Failed to find consensus orientation after "
-                                   f"{iters} iterations. Best guess is the closest match: {best[j]}")
                 out.append(OrientationResult(
                     query_vector=qv[s0 + j].squeeze().astype(np.float64),
                     best_orientation=best[j], mean_orientation=mean[j] if succ else None,
-                    candidate_orientations=self._orientations[idx[j]], distances=scores[j],
+                    candidate_orientations=cands[j], distances=scores[j],
                     success=succ, similar_indices=sim))
         return out
 
@@ -232,7 +273,7 @@ class FaissLatentVectorDatabase:
 
     # ------------------------------------------------------------------ bookkeeping
     def get_count(self) -> int:
-        return int(self._db.shape[0])
+        return int(self._n)
 
     @property
     def orientations(self) -> np.ndarray:
@@ -255,15 +296,13 @@ class FaissLatentVectorDatabase:
                 raise ValueError(f"{path} has no 'latents' array (a faiss-serialised index "
                                  "needs faiss to read; re-create it with add_vectors)")
             lv = data["latents"].astype(np.float32)
-            self._orientations = data["orientations"].astype(np.float64).reshape(-1, 3)
+            ori = data["orientations"].astype(np.float64).reshape(-1, 3)
         self.dimension = lv.shape[1]
-        self._db = torch.from_numpy(lv).to(self.device)
-        self._ori_dev = torch.from_numpy(self._orientations).to(self.device)
+        self._reset(lv.shape[0])
+        self._append(torch.from_numpy(lv).to(self.device), ori)
 
     def delete_persistence(self) -> None:
         """faiss_db.py:468-496."""
         if self.npz_path.exists():
             self.npz_path.unlink()
-            self._db = torch.empty(0, self.dimension, dtype=torch.float32, device=self.device)
-            self._orientations = np.empty((0, 3), dtype=np.float64)
-            self._ori_dev = torch.empty(0, 3, dtype=torch.float64, device=self.device)
+            self._reset()

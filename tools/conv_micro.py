@@ -31,6 +31,7 @@ CASES = {
     "dgrad32": ("dgrad", 128, 32, 32, P_ID),
     "dgrad64": ("dgrad", 64, 64, 64, P_ID),
     "wgrad32": ("wgrad", 128, 32, 32, ACT_NORM),
+    "wgrad32u": ("wgrad", 128, 32, 32, ACT_NORM_UP),
     "wgrad64": ("wgrad", 64, 64, 64, ACT_NORM),
     "wgrad128": ("wgrad", 32, 128, 128, ACT_NORM),
 }
@@ -76,7 +77,8 @@ def run(name, reps, pieces, B, warm=1.0):
             N.call("ebsdvae_conv3x3_dgrad_inbwd_split", gy.data_ptr(), wp.data_ptr(), gin.data_ptr(),
                    yprev.data_ptr(), stp.data_ptr(), mode, part.data_ptr(), B, H, H, cout, cin, pieces, s)
     else:
-        src = torch.randn(B, H, H, cin, device=dev, generator=g)
+        Hs = H // 2 if mode == ACT_NORM_UP else H
+        src = torch.randn(B, Hs, Hs, cin, device=dev, generator=g)
         st = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
         gy = torch.randn(B, H, H, cout, device=dev, generator=g)
         S_ = N.call("ebsdvae_conv3x3_wgrad_split_slices", B, H, H, cin, cout, pieces)
