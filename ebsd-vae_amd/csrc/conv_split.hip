@@ -388,7 +388,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 //     next iteration (after the barrier), so its stores drain under the next tile's MFMAs.
 // The old kernel paid each of these serially: one exposed global-load latency and one VALU
 // staging phase per chunk, plus the prologue / epilogue per tile (tools/conv_micro.py).
-template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP>
+template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI>
 __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, const char* __restrict__ wp,
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
@@ -408,8 +408,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr int PD = POOL ? 1 : 2;               // halo prefetch distance (iterations)
   static_assert(PD == 1 || KX * NR <= 7, "pipe_barrier keeps at most 7 loads in flight");
   extern __shared__ __attribute__((aligned(16))) char xsm[];
+  // a tile is TH rows of one image, or NI whole images (NI > 1: TH == H); NI is a template
+  // parameter so the single-image kernels carry none of the per-image bookkeeping
   const int HP = TH + 2, WP = W + 2;
-  const int pixP = HP * WP;
+  const int pixI = HP * WP;            // halo pixels per image of the tile
+  const int pixP = NI * pixI;
   const int xslab = (pixP + 1) * XPS;
   char* lw0 = xsm;
   char* lx0 = xsm + 2 * WSLABP;
@@ -421,15 +424,16 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   const int tpx = TH * W;
   const int nch = Cin / XCK;
   const int t0 = blockIdx.x * tpb;
-  const int ntl = min(tpb, B * tpi - t0);
+  const int ntl = min(tpb, ((B + NI - 1) / NI) * tpi - t0);
   const int nit = ntl * nch;
 
   int abase[MF];
 #pragma unroll
   for (int mf = 0; mf < MF; ++mf) {
     const int p = wm * MW + mf * 32 + l32;
-    const int r = p / W, c = p - r * W;
-    abase[mf] = r * WP + c;
+    const int im = p / tpx, pr = p - im * tpx;
+    const int r = pr / W, c = pr - r * W;
+    abase[mf] = im * pixI + r * WP + c;
   }
   int toff[5];
 #pragma unroll
@@ -441,6 +445,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   const int Hs = POOL ? 2 * H : (UPS ? H / 2 : H);
   const int Ws = POOL ? 2 * W : (UPS ? W / 2 : W);
   const int q = tid & 1;
+  // halo items: image img_w = wave / WPI of the tile is staged by its own WPI waves (so the
+  // IN statistics a wave needs are one image's: wave-uniform); half-item hi of the group
+  constexpr int WPI = NWV / NI;
+  static_assert(NWV % NI == 0, "waves split evenly over the tile's images");
+  const int img_w = wave / WPI;
+  const int tig = tid - img_w * WPI * 64;
   // tile-invariant item geometry: hm1 = halo row - 1 (a large negative sentinel past the halo
   // or in a padding column), boff = the item's byte offset in its source image relative to the
   // tile's first row (0x80000000 = always out of range), ldo = its LDS record offset
@@ -448,26 +458,29 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   const int rowb = Ws * Cin * 4;   // bytes per source row
 #pragma unroll
   for (int k = 0; k < KX; ++k) {
-    const int pix = (tid + NTHR * k) >> 1;
-    const int hh = pix / WP, ww = pix - hh * WP;
-    const bool in = pix < pixP && ww >= 1 && ww <= W;
+    const int pixl = (tig + WPI * 64 * k) >> 1;   // pixel within this image's halo
+    const int pix = img_w * pixI + (pixl < pixI ? pixl : pixP);
+    const int hh = pixl / WP, ww = pixl - hh * WP;
+    const bool in = pixl < pixI && ww >= 1 && ww <= W;
     const int r = hh - 1, c = ww - 1;
     int o;
     if (POOL) o = 2 * r * rowb + 2 * c * Cin * 4;
     else if (UPS) o = (r >> 1) * rowb + (c >> 1) * Cin * 4;
     else o = r * rowb + c * Cin * 4;
     hm1[k] = in ? r : -(1 << 28);
-    boff[k] = in ? o + q * 16 : (int)0x80000000;
+    boff[k] = in ? o + img_w * (Hs * Ws * Cin * 4) + q * 16 : (int)0x80000000;
 #ifdef EV_X_CONTIG   // timing experiment only: contiguous halo bytes (wrong results)
     boff[k] = in ? (pix * 32 + q * 16) : (int)0x80000000;
 #endif
-    ldo[k] = (pix < pixP ? pix : pixP) * XPS + q * 8;
+    ldo[k] = (pixl < pixI ? pix : pixP) * XPS + q * 8;
   }
   const int img_bytes = Hs * Ws * Cin * 4;
   // item k of this wave holds at least one halo pixel (wave index made provably uniform so
   // the test is a scalar branch)
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  auto item_live = [&](int k) EV_LAMBDA_INLINE { return (wave_u * 64 + NTHR * k) < 2 * pixP; };
+  const int tig_u = __builtin_amdgcn_readfirstlane(tig - (tid & 63));   // the wave's first lane
+  const int img_u = __builtin_amdgcn_readfirstlane(img_w);
+  auto item_live = [&](int k) EV_LAMBDA_INLINE { return (tig_u + WPI * 64 * k) < 2 * pixI; };
 
   float4 raw[PD][KX][NR];
   float2 st[PD][4];
@@ -478,8 +491,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const int tl = it / nch;
     ch = it - tl * nch;
     const int t = t0 + tl;
-    b0 = t / tpi;
-    h0 = (t - b0 * tpi) * TH;
+    const int grp = t / tpi;
+    b0 = grp * NI;
+    h0 = (t - grp * tpi) * TH;
   };
   // halo loads of iteration it into register slot sl: buffer loads with 32-bit offsets into
   // the tile's source image; rows above / below the image fall outside the descriptor's range
@@ -490,7 +504,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     coords(it, b0, h0, ch);
     sb0[sl] = b0; sh0[sl] = h0; sch[sl] = ch;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)b0 * Hs * Ws * Cin), 0,
-                                                      img_bytes, 0x00020000);
+                                                      NI == 1 ? img_bytes : img_bytes * min(NI, B - b0),
+                                                      0x00020000);
 #ifdef EV_X_CONTIG
     const int toff = h0 * rowb + ch * (pixP * 32);
 #else
@@ -514,7 +529,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     if (NORM) {
       // the chunk's 8 {mean, rstd} pairs are wave-uniform: one scalar-cache load (no TA
       // traffic), then each lane keeps its 4-channel half
-      const float4* sp = reinterpret_cast<const float4*>(sstats + (size_t)b0 * Cin + ch * XCK);
+      const int bs = NI == 1 ? b0 : min(b0 + img_u, B - 1);   // this wave's image
+      const float4* sp = reinterpret_cast<const float4*>(sstats + (size_t)bs * Cin + ch * XCK);
       const float4 u0 = sp[0], u1 = sp[1], u2 = sp[2], u3 = sp[3];
       const float4 s01 = q ? u2 : u0, s23 = q ? u3 : u1;
       st[sl][0] = make_float2(s01.x, s01.y); st[sl][1] = make_float2(s01.z, s01.w);
@@ -534,10 +550,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const bool ok = (okm[sl] >> k) & 1;
     v = make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
     if (act_out) {   // uniform: materialise the (pooled) activation for the wgrad
-      const int pix = (tid + NTHR * k) >> 1;
-      const int hh = pix / WP, gw = pix - hh * WP - 1;
-      if (ok && hh >= 1 && hh <= TH && gw >= 0 && gw < W)
-        st4(act_out + (((size_t)sb0[sl] * H + sh0[sl] + hh - 1) * W + gw) * Cin + sch[sl] * XCK + q * 4, v);
+      const int pixl = (tig + WPI * 64 * k) >> 1;
+      const int hh = pixl / WP, gw = pixl - hh * WP - 1;
+      if (ok && hh >= 1 && hh <= TH && gw >= 0 && gw < W &&
+          (NI == 1 || (pixl < pixI && sb0[sl] + img_w < B)))
+        st4(act_out + (((size_t)(sb0[sl] + img_w) * H + sh0[sl] + hh - 1) * W + gw) * Cin +
+                sch[sl] * XCK + q * 4, v);
     }
     bf16x4 pc[NP];
     split4<NP>(v, pc);
@@ -577,8 +595,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   auto epilogue = [&](int it_done) EV_LAMBDA_INLINE {
     int b0, h0, ch;
     coords(it_done, b0, h0, ch);
-    pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0, h0, wm * MW, wn * NF * 32, hk, l32,
-                                  yprev, stprev, ipart);
+    const int im = NI == 1 ? 0 : (wm * MW) / tpx;   // the wave's pixels lie in one image
+    if (NI == 1 || b0 + im < B)
+      pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wm * MW - im * tpx,
+                                    wn * NF * 32, hk, l32, yprev, stprev, ipart);
   };
 
 #ifdef EV_PIPE_TRACE
@@ -747,6 +767,15 @@ static bool use_pipe() {
   return v != 0;
 }
 
+// EBSDVAE_CONV_MULTI_IMAGE=0: 8x8 maps go to the fp32 small-map kernels (A/B timing)
+static bool use_multi_image() {
+  static const int v = [] {
+    const char* e = getenv("EBSDVAE_CONV_MULTI_IMAGE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v != 0;
+}
+
 // compute units of the current device (cached per device id)
 static int cu_count() {
   static int cache[64] = {0};
@@ -763,6 +792,7 @@ static int cu_count() {
 
 struct X3Cfg {
   int M, TH, NT, KX, nwv;
+  int NI;            // images per tile (> 1 only for the pipelined kernel on small maps)
   size_t lds;        // conv3x3_split_kernel
   size_t lds_pipe;   // conv3x3_pipe_kernel (padded weight buffers); 0 = does not fit
 };
@@ -773,29 +803,42 @@ struct X3Cfg {
 static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   if ((np != 2 && np != 3) || cin % (2 * XCK) || !(cout == 128 || cout == 64 || cout == 32)) return false;
   c->M = (np == 3 && cout != 128) ? 512 : 256;
-  if (H * W < c->M || W > c->M || c->M % W) return false;
-  c->TH = c->M / W;
-  if (H % c->TH) return false;
+  c->NI = 1;
   c->NT = cout;
   c->nwv = (cout == 128 || np == 3) ? 8 : 4;
-  const int pix = (c->TH + 2) * (W + 2);
-  c->KX = (pix * 2 + c->nwv * 64 - 1) / (c->nwv * 64);
+  if (H * W < c->M) {
+    // 8x8 maps (bf16x6, 128 channels): tiles of two whole images, 128 pixels, 8 waves of
+    // 64 px x 32 co; pipelined kernel only
+    if (!(np == 3 && cout == 128 && H * W == 64 && use_pipe() && use_multi_image())) return false;
+    c->M = 128;
+    c->NI = 2;
+    c->TH = H;
+  } else {
+    if (W > c->M || c->M % W) return false;
+    c->TH = c->M / W;
+    if (H % c->TH) return false;
+  }
+  const int pixI = (c->TH + 2) * (W + 2);
+  const int pix = c->NI * pixI;
+  const int tpg = (c->nwv / c->NI) * 64;   // threads staging one image's halo
+  c->KX = (pixI * 2 + tpg - 1) / tpg;
   const int kxmax = np == 2 ? (cout == 128 ? 2 : (cout == 64 ? 5 : 7)) : (cout == 128 ? 2 : (cout == 64 ? 4 : 5));
   if (c->KX > kxmax) return false;
   const int wslab = XTAPS * np * cout * 16;
   c->lds = 2 * (size_t)wslab + 2 * (size_t)(pix + 1) * XPS;
   c->lds_pipe = 2 * (size_t)pipe_dma_per(wslab, c->nwv) * c->nwv * 1024 + 2 * (size_t)(pix + 1) * XPS;
   if (c->lds_pipe > 160 * 1024) c->lds_pipe = 0;
+  if (c->NI > 1) return c->lds_pipe != 0;   // no non-persistent form for multi-image tiles
   return c->lds <= 160 * 1024;
 }
 
-template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP>
+template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI>
 static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const void* wp,
                         const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                         int cin, hipStream_t s, const InBwdFuse& f) {
-  const int ntiles = B * (H / c.TH);
-  if (use_pipe() && c.lds_pipe) {
-    auto k = conv3x3_pipe_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP>;
+  const int ntiles = ((B + NI - 1) / NI) * (H / c.TH);
+  if (NI > 1 || (use_pipe() && c.lds_pipe)) {
+    auto k = conv3x3_pipe_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP, NI>;
     static bool once = false;
     if (!once) {
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -810,35 +853,37 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
                        f.stprev, f.part);
     return;
   }
-  auto k = conv3x3_split_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP>;
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    once = true;
+  if constexpr (NI == 1) {
+    auto k = conv3x3_split_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP>;
+    static bool once = false;
+    if (!once) {
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      once = true;
+    }
+    hipLaunchKernelGGL(k, dim3(ntiles), dim3(NWV * 64), c.lds, s, src, (const float2*)st,
+                       (const char*)wp, bias, y, (float2*)part, aout, B, H, W, cin, c.TH, f.yprev,
+                       f.stprev, f.part);
   }
-  hipLaunchKernelGGL(k, dim3(ntiles), dim3(NWV * 64), c.lds, s, src, (const float2*)st,
-                     (const char*)wp, bias, y, (float2*)part, aout, B, H, W, cin, c.TH, f.yprev,
-                     f.stprev, f.part);
 }
 
-template <int NP, int NWV, int WM, int MF, int NF, int KX>
+template <int NP, int NWV, int WM, int MF, int NF, int KX, int NI = 1>
 static void launch_x3(const X3Cfg& c, const float* src, const float* st, int mode, const void* wp,
                       const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                       int cin, hipStream_t s, int pmode, const InBwdFuse& f) {
   if (pmode >= 0) {
     switch (pmode) {
-      case P_ID: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_ID>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
-      case P_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_POOL>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
-      default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_UP>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+      case P_ID: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_ID, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+      case P_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_POOL, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+      default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_UP, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
     }
     return;
   }
   switch (mode) {
-    case ACT_RAW: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    case ACT_NORM: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    case ACT_NORM_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_POOL, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    case ACT_UP: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_UP, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_UP, FP_NONE>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_RAW: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_NORM: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_NORM_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_POOL, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_UP: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_UP, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_UP, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
   }
 }
 
@@ -854,7 +899,9 @@ static void dispatch_split(const X3Cfg& c, int np, const float* src, const float
     else
       launch_x3<2, 4, 4, 2, 1, 7>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
   } else {
-    if (cout == 128)
+    if (cout == 128 && c.NI > 1)   // two 8x8 images per tile: 2 x 4 waves of 64 px x 32 co
+      launch_x3<3, 8, 2, 2, 1, 1, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else if (cout == 128)
       launch_x3<3, 8, 4, 2, 2, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 64)
       launch_x3<3, 8, 8, 2, 2, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);

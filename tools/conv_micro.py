@@ -18,7 +18,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "ebsd-vae_amd")]
 import torch  # noqa: E402
 
 from latice import _native as N  # noqa: E402
-from latice.engine import ACT_NORM, ACT_NORM_POOL, ACT_NORM_UP, P_ID, P_POOL  # noqa: E402
+from latice.engine import ACT_NORM, ACT_NORM_POOL, ACT_NORM_UP, P_ID, P_POOL, P_UP  # noqa: E402
 
 # name: (kind, H, cin, cout, src_mode / pmode)
 CASES = {
@@ -30,6 +30,7 @@ CASES = {
     "fwd64to32u": ("fwd", 128, 64, 32, ACT_NORM_UP),
     "dgrad32": ("dgrad", 128, 32, 32, P_ID),
     "dgrad64": ("dgrad", 64, 64, 64, P_ID),
+    "dgrad32u": ("dgrad", 128, 32, 32, P_UP),
     "wgrad32": ("wgrad", 128, 32, 32, ACT_NORM),
     "wgrad32u": ("wgrad", 128, 32, 32, ACT_NORM_UP),
     "wgrad64": ("wgrad", 64, 64, 64, ACT_NORM),
@@ -63,7 +64,7 @@ def run(name, reps, pieces, B, warm=1.0):
         # input gradient of a cin->cout layer: a conv cout->cin, fused reduce of the block
         # feeding it (y_prev at 2H for P_POOL)
         gy = torch.randn(B, H, H, cout, device=dev, generator=g)
-        Hp = 2 * H if mode == P_POOL else H
+        Hp = 2 * H if mode == P_POOL else (H // 2 if mode == P_UP else H)
         yprev = torch.randn(B, Hp, Hp, cin, device=dev, generator=g)
         stp = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
         wp = torch.empty(N.call("ebsdvae_pack_split_bytes", cout, cin, pieces) // 4, device=dev)
