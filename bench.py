@@ -10,7 +10,10 @@ One "step" = forward (encoder -> reparameterise -> decoder) + BCE/KL loss + back
 Prints ONE JSON line (rank 0) with the driver's contract fields plus:
   roofline      the dominant kernel family (by GPU time), its algorithmic FLOPs per
                 launch / average launch duration (HIP events on the launch stream, live in
-                the timed region) against the fp32 MFMA peak (157.3 TFLOP/s);
+                the timed region on every --probe-every'th step) against the peak of the
+                conv arithmetic (bf16 MFMA / products per fp32 product, or fp32 MFMA);
+  c5_256        the c5 configuration (256x256, latent 64, batch 128/GPU) step rate;
+  c4_encoder_latents  build_dictionary throughput and a batched query;
   cpu_baseline  oracle/torch_port.py (PyTorch-CPU restatement of the reference
                 training_step) timed on this host's cores on a bounded sample (N=1, rank 0).
 """
@@ -165,6 +168,46 @@ def encoder_latents(model, plan, args, dev, world):
                       "ms": round(qel * 1e3, 3)}}
 
 
+def c5_step_rate(args, dev, world, rank):
+    """BASELINE c5: the same training step on 256x256 patterns, latent 64, batch 128 per GPU
+    (SURVEY.md section 8: per-GPU 128, global 128*N), weak scaling like the headline line;
+    barrier + synchronize around the timed steps, max over ranks."""
+    from latice.model import VariationalAutoEncoderRawData
+    from latice.seeding import seeded_state_dict, synthetic_patterns
+    from latice.trainer import VAETrainer
+    S, L, B = 256, 64, 128
+    model = VariationalAutoEncoderRawData(32, L, S)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in seeded_state_dict(5, 32, L, S).items()})
+    model = model.to(dev)
+    trainer = VAETrainer(model, kl_lambda=5e-6, lr=1e-4, seed=2000 + rank)
+    x = torch.from_numpy(synthetic_patterns(100 + rank, B, S)).to(dev)
+    for _ in range(3):
+        trainer.step(x)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.c5_steps):
+        out = trainer.step(x)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    loss = float(out[0])
+    step_tflops = step_flops_per_pattern(model.plan) * B * args.c5_steps / el / 1e12
+    del trainer, model, x
+    torch.cuda.empty_cache()
+    return {"metric": "EBSD patterns/sec (256x256, latent 64, fwd+bwd)",
+            "value": round(world * B * args.c5_steps / el, 2), "unit": "patterns/s",
+            "batch_per_gpu": B, "global_batch": world * B, "steps": args.c5_steps,
+            "ms_per_step": round(el / args.c5_steps * 1e3, 3),
+            "step_fp32_tflops": round(step_tflops, 2), "loss_finite": bool(np.isfinite(loss))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,10 +220,14 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
+    ap.add_argument("--probe-every", type=int, default=5,
+                    help="bracket the conv launches with HIP events on every k-th timed step")
     ap.add_argument("--precision", default=None, choices=["fp32", "bf16x6", "bf16x3"],
                     help="conv arithmetic (default: the engine default, bf16x6)")
     ap.add_argument("--c4-batches", type=int, default=1024,
                     help="encoder-only inference batches of 1024 for the c4 latents/s field (0: skip)")
+    ap.add_argument("--c5-steps", type=int, default=10,
+                    help="timed steps of the c5 leg (256x256, latent 64, batch 128/GPU; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -224,12 +271,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if probe is not None:
-        with probe:
-            for _ in range(args.steps):
+    probed = 0
+    for i in range(args.steps):
+        if probe is not None and i % args.probe_every == 0:
+            # event-bracketed launches on a sample of the timed steps: each event pair costs
+            # the stream a few microseconds, so bracketing every launch of every step would
+            # slow the step the value is quoted on by ~2 %
+            with probe:
                 out = trainer.step(x)
-    else:
-        for _ in range(args.steps):
+            probed += 1
+        else:
             out = trainer.step(x)
     torch.cuda.synchronize()
     if world > 1:
@@ -258,8 +309,9 @@ def main():
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
                 "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": pmc_traffic(dom),
-                "launches_per_step": d["launches"] // args.steps,
-                "split_bf16_launches_per_step": d["split_launches"] // args.steps,
+                "launches_per_step": d["launches"] // probed,
+                "split_bf16_launches_per_step": d["split_launches"] // probed,
+                "probed_steps": probed,
                 "avg_launch_us": round(avg_s * 1e6, 2),
                 "gflop_per_launch": round(flops_per_launch / 1e9, 3),
                 "flops": "algorithmic fp32-equivalent (2*B*H*W*Cin*Cout*9 per conv)"}
@@ -286,8 +338,10 @@ def main():
         "step_fp32_tflops": round(step_tflops, 2),
         "step_frac_of_fp32_peak": round(step_tflops / FP32_PEAK_TFLOPS, 4),
         "loss": round(loss, 6),
-        "kernel_families_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in fam.items()},
+        "kernel_families_ms_per_step": {k: round(v["ms"] / max(1, probed), 3) for k, v in fam.items()},
     }
+    if args.c5_steps > 0 and args.image_size == 128:
+        res["c5_256"] = c5_step_rate(args, dev, world, rank)
     if args.c4_batches > 0:
         res["c4_encoder_latents"] = encoder_latents(model, plan, args, dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
