@@ -17,6 +17,9 @@ EV_DEVINL void glds16(const float* g, float* lds_wave_base) {
 
 // ------------------------------------------------------------------ shared epilogue
 constexpr int FP_NONE = -1;   // no fused InstanceNorm-backward reduce
+// forward of a layer whose output the next layer max-pools (pipelined split kernel only):
+// the epilogue also writes the 2x2 max of the raw output y at (H/2, W/2)
+constexpr int FP_POOLOUT = 3;
 
 // Fused InstanceNorm-backward reduce of the PREVIOUS block (input-gradient convs only):
 // this conv's output is g = d loss / d a_prev (a_prev = [pool|up](lrelu(IN(y_prev))) at
@@ -138,6 +141,7 @@ struct InBwdFuse {
   const float* yprev = nullptr;
   const float2* stprev = nullptr;
   double2* part = nullptr;
+  float* ypool = nullptr;   // FP_POOLOUT forward: the max-pooled raw output
 };
 
 }  // namespace ev

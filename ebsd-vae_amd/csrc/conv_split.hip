@@ -295,15 +295,17 @@ EV_DEVINL void pipe_barrier() {
 // Epilogue of conv3x3_pipe_kernel: conv_epilogue (conv_common.h) for one tile of one image,
 // with 32-bit buffer offsets instead of 64-bit addresses (the same values, the same
 // summation order, so results are bit-identical to the non-persistent kernel's).
+//   wpx0  tile pixel of the wave's first fragment, mfs the pixel stride between its fragments
+//         (32: one contiguous run; W: FP_POOLOUT's row pairs), slot its statistics slot
+//   ypool FP_POOLOUT: the (H/2, W/2) max-pooled raw output (2x2 windows are lane-local)
 template <int MF, int NF, int FP, int NT>
 EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bias,
                              float* __restrict__ y, float2* __restrict__ spart, int H, int W, int b0,
-                             int h0, int wpx0, int co_base, int hk, int l32,
+                             int h0, int wpx0, int mfs, int slot, int co_base, int hk, int l32,
                              const float* __restrict__ yprev, const float2* __restrict__ stprev,
-                             double2* __restrict__ ipart) {
+                             double2* __restrict__ ipart, float* __restrict__ ypool) {
   constexpr int MW = MF * 32;
   const int T = (H * W) / MW;
-  const int slot = (h0 * W + wpx0) / MW;
   const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ((size_t)b0 * H + h0) * W * NT), 0,
                                                     0x7fffffff, 0x00020000);
 #pragma unroll
@@ -320,9 +322,41 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         acc[mf][nf][r] = v;
         s += v;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
-                                              vbase + (mf * 32 + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
+                                              vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
       }
-    if (FP != FP_NONE) {
+    if (FP == FP_POOLOUT) {
+      // max(lrelu(IN(y))) over a window == lrelu(IN(max y)) (IN's scale is positive, both maps
+      // are monotone), so the consumer reads this tensor in ACT_NORM mode with y's statistics
+      static_assert(MF == 2, "row-pair fragments");
+      const int W2 = W >> 1;
+      const auto rq = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(ypool + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
+      if (W >= 32) {   // fragment 0 = tile row 2rp, fragment 1 = row 2rp + 1, same 32 columns
+        const int prow = wpx0 / W >> 1, pcol = (wpx0 % W + 4 * hk) >> 1;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const float m = fmaxf(fmaxf(acc[0][nf][r], acc[0][nf][r + 1]),
+                                fmaxf(acc[1][nf][r], acc[1][nf][r + 1]));
+          const int pc = pcol + (((r & 3) + 8 * (r >> 2)) >> 1);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
+                                                ((prow * W2 + pc) * NT + co) * 4, 0, 0);
+        }
+      } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf) {
+          const int prow = (wpx0 + mf * mfs) / W >> 1;
+#pragma unroll
+          for (int r = 0; r < 8; r += 2) {
+            const float m = fmaxf(fmaxf(acc[mf][nf][r], acc[mf][nf][r + 1]),
+                                  fmaxf(acc[mf][nf][r + 8], acc[mf][nf][r + 9]));
+            const int pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
+                                                  ((prow * W2 + pc) * NT + co) * 4, 0, 0);
+          }
+        }
+      }
+    }
+    if (FP != FP_NONE && FP != FP_POOLOUT) {
       constexpr int NL = FP == P_POOL ? 4 : 1;
       constexpr int GM = NF == 1 ? 32 : EV_PIPE_EPI_G;   // loads in flight per batch
       constexpr int G = (GM / NL) < MF * 16 ? (GM / NL) : MF * 16;
@@ -393,11 +427,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, const char* __restrict__ wp,
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
     float* __restrict__ act_out, int B, int H, int W, int Cin, int TH, int tpb,
-    const float* __restrict__ yprev, const float2* __restrict__ stprev, double2* __restrict__ ipart) {
+    const float* __restrict__ yprev, const float2* __restrict__ stprev, double2* __restrict__ ipart,
+    float* __restrict__ ypool) {
   constexpr int WN = NWV / WM;
   constexpr int NT = WN * NF * 32;               // == Cout
   constexpr int MW = MF * 32;
-  constexpr int NTHR = NWV * 64;
   constexpr int WSLAB = XTAPS * NP * NT * 16;
   constexpr int WPER = pipe_dma_per(WSLAB, NWV);  // 1-KiB weight pieces per wave per chunk
   constexpr int WSLABP = WPER * NWV * 1024;       // LDS weight buffer (padded to whole rounds)
@@ -427,10 +461,20 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   const int ntl = min(tpb, ((B + NI - 1) / NI) * tpi - t0);
   const int nit = ntl * nch;
 
+  // the wave's fragments: tile pixel of the first (fpx0) and the stride between them (mfs).
+  // FP_POOLOUT on W >= 32 pairs rows (fragment 0 = row 2rp, fragment 1 = row 2rp + 1 of the
+  // same 32 columns) so every 2x2 pooling window is lane-local; otherwise one contiguous run
+  // (for W == 16 the window is already inside a fragment)
+  int fpx0 = wm * MW, mfs = 32;
+  if (FP == FP_POOLOUT && W >= 32) {
+    const int cbs = W >> 5, rp = wm / cbs;
+    fpx0 = 2 * rp * W + (wm - rp * cbs) * 32;
+    mfs = W;
+  }
   int abase[MF];
 #pragma unroll
   for (int mf = 0; mf < MF; ++mf) {
-    const int p = wm * MW + mf * 32 + l32;
+    const int p = fpx0 + mf * mfs + l32;
     const int im = p / tpx, pr = p - im * tpx;
     const int r = pr / W, c = pr - r * W;
     abase[mf] = im * pixI + r * WP + c;
@@ -596,9 +640,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     int b0, h0, ch;
     coords(it_done, b0, h0, ch);
     const int im = NI == 1 ? 0 : (wm * MW) / tpx;   // the wave's pixels lie in one image
+    const int wpx0 = fpx0 - im * tpx;
     if (NI == 1 || b0 + im < B)
-      pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wm * MW - im * tpx,
-                                    wn * NF * 32, hk, l32, yprev, stprev, ipart);
+      pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
+                                    (h0 * W + wm * MW - im * tpx) / MW, wn * NF * 32, hk, l32,
+                                    yprev, stprev, ipart, ypool);
   };
 
 #ifdef EV_PIPE_TRACE
@@ -850,10 +896,10 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
     const int nblk = (ntiles + tpb - 1) / tpb;
     hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), c.lds_pipe, s, src, (const float2*)st,
                        (const char*)wp, bias, y, (float2*)part, aout, B, H, W, cin, c.TH, tpb, f.yprev,
-                       f.stprev, f.part);
+                       f.stprev, f.part, f.ypool);
     return;
   }
-  if constexpr (NI == 1) {
+  if constexpr (NI == 1 && FP != FP_POOLOUT) {
     auto k = conv3x3_split_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP>;
     static bool once = false;
     if (!once) {
@@ -877,6 +923,12 @@ static void launch_x3(const X3Cfg& c, const float* src, const float* st, int mod
       default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_UP, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
     }
     return;
+  }
+  if constexpr (NI == 1) {
+    if (f.ypool) {   // producer of a max-pooled layer (ebsdvae_conv3x3_fwd_split_pooled)
+      launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM, FP_POOLOUT, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f);
+      return;
+    }
   }
   switch (mode) {
     case ACT_RAW: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
@@ -971,6 +1023,31 @@ extern "C" int ebsdvae_conv3x3_fwd_split(const float* src, const float* src_stat
   dispatch_split(c, pieces, src, src_stats, src_mode, wpack, bias, y, stat_part, act_out, B, H, W,
                  cin, cout, (hipStream_t)stream, -1, InBwdFuse());
   return evh::check_launch("conv3x3_fwd_split");
+}
+
+extern "C" int ebsdvae_conv3x3_split_pool_ok(int H, int W, int cin, int cout, int pieces) {
+  X3Cfg c;
+  return (plan_split(H, W, cin, cout, pieces, &c) && use_pipe() && c.lds_pipe && c.NI == 1 &&
+          c.TH % 2 == 0 && W >= 16 && (W & (W - 1)) == 0) ? 1 : 0;
+}
+
+extern "C" int ebsdvae_conv3x3_fwd_split_pooled(const float* src, const float* src_stats,
+                                                int src_mode, const void* wpack, const float* bias,
+                                                float* y, float* ypool, float* stat_part, int B,
+                                                int H, int W, int cin, int cout, int pieces,
+                                                ebsdvae_stream_t stream) {
+  X3Cfg c;
+  EV_REQUIRE(src && src_stats && wpack && y && ypool && stat_part && B > 0,
+             "conv3x3_fwd_split_pooled: null pointer or empty batch");
+  EV_REQUIRE(src_mode == ACT_NORM, "conv3x3_fwd_split_pooled: src_mode %d (ACT_NORM only)", src_mode);
+  EV_REQUIRE(ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, pieces) && plan_split(H, W, cin, cout, pieces, &c),
+             "conv3x3_fwd_split_pooled: unsupported shape H=%d W=%d cin=%d cout=%d pieces=%d", H, W,
+             cin, cout, pieces);
+  InBwdFuse f;
+  f.ypool = ypool;
+  dispatch_split(c, pieces, src, src_stats, src_mode, wpack, bias, y, stat_part, nullptr, B, H, W,
+                 cin, cout, (hipStream_t)stream, -1, f);
+  return evh::check_launch("conv3x3_fwd_split_pooled");
 }
 
 extern "C" int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpack, float* gin,

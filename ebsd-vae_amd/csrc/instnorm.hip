@@ -334,7 +334,10 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
   }
   __syncthreads();
   const int p0 = tile * rows * W, p1 = p0 + rows * W;
-#pragma unroll 2
+  // the FINAL reduce pass is VALU-heavy (9-tap recompute + 36 weight-gradient FMAs per
+  // pixel): 2 pixels in flight per thread; the others stream and keep 4
+  constexpr int UNR = (FUSE == FUSE_FINAL && !APPLY) ? 2 : 4;
+#pragma unroll UNR
   for (int p = p0 + pr; p < p1; p += NPR) {
     const int h = p / W, w = p - h * W;
     float nb[9];   // FINAL: g1[q - d(tap)] ; FIRST: x[p + d(tap)]
@@ -525,7 +528,10 @@ extern "C" int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* 
                                     int H, int W, int C, ebsdvae_stream_t stream) {
   EV_REQUIRE(gnext && y && stats && bstats && gy, "in_bwd_apply: null pointer");
   EV_REQUIRE(pmode >= 0 && pmode <= 2 && C % 4 == 0 && (256 % (C / 4)) == 0, "in_bwd_apply: bad pmode/C");
-  const int T = in_bwd_tiles_host(H, W);
+  // the apply pass keeps no per-tile partials: split the planes finer than the reduce so
+  // small maps still put >= 2048 workgroups (8 per CU) in flight
+  int T = in_bwd_tiles_host(H, W);
+  while (B * T < 2048 && H % (2 * T) == 0 && ((H / (2 * T)) & 1) == 0) T *= 2;
   hipLaunchKernelGGL(in_bwd_kernel<true>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
                      pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy, H,
                      W, C, T);

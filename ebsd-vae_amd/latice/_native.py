@@ -35,6 +35,8 @@ SIGNATURES = {
     "ebsdvae_pack_split_bytes": [I, I, I],
     "ebsdvae_pack_conv_weights_split": [P, I, I, P],
     "ebsdvae_conv3x3_fwd_split": [P, P, I, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_split_pool_ok": [I, I, I, I, I],
+    "ebsdvae_conv3x3_fwd_split_pooled": [P, P, I, P, P, P, P, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_dgrad_inbwd_split": [P, P, P, P, P, I, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_fwd": [P, P, I, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],
@@ -84,6 +86,7 @@ QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgr
            "ebsdvae_wgrad_reduce_batch_work", "ebsdvae_cosine_topk_work",
            "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
+           "ebsdvae_conv3x3_split_pool_ok",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices"}
 
 _lib = None

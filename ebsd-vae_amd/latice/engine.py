@@ -288,11 +288,25 @@ class PackSet:
         return self.packs
 
 
-def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=None):
+def pool_out_ok(layer: ConvLayer, wp) -> bool:
+    """The layer's split conv can also emit its max-pooled raw output (FP_POOLOUT).
+    EBSDVAE_POOL_OUT=0 turns the pooled hand-off off (A/B timing)."""
+    if os.environ.get("EBSDVAE_POOL_OUT", "1") == "0":
+        return False
+    return bool(wp is not None and wp.pieces and N.call(
+        "ebsdvae_conv3x3_split_pool_ok", layer.H, layer.H, layer.cin, layer.cout, wp.pieces))
+
+
+def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=None, mode=None,
+                 pool_out=False):
     """One conv block forward: y (B,H,H,cout) pre-norm + IN stats {mean,rstd} (B,cout,2).
     keep_act: also return the conv's logical input (materialised by the kernel), used by
-    max-pool-fed layers so their wgrad reads the pooled tensor.  wp: pre-packed weight."""
+    max-pool-fed layers so their wgrad reads the pooled tensor.  wp: pre-packed weight.
+    mode: source mode override (a max-pool-fed layer reading its producer's pooled output
+    in ACT_NORM mode).  pool_out: also return ypool = 2x2 max of y (B,H/2,H/2,cout), the
+    producer side of that (ebsdvae_conv3x3_fwd_split_pooled)."""
     H = layer.H
+    src_mode = layer.src_mode if mode is None else mode
     if wp is None:
         wp = pack_weight(w, layer, dgrad=False)
     y = _empty(B, H, H, layer.cout, like=w)
@@ -301,10 +315,17 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     part = _empty(B, T, layer.cout, 2, like=w)
     act = _empty(B, H, H, layer.cin, like=w) if keep_act else None
     tag = f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m{layer.src_mode}"
-    args = (N.ptr(src), N.ptr(src_stats), layer.src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y),
+    args = (N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y),
             N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout)
     flops = conv_flops(B, H, H, layer.cin, layer.cout)
-    if wp.pieces:
+    ypool = None
+    if pool_out:
+        ypool = _empty(B, H // 2, H // 2, layer.cout, like=w)
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split_pooled", N.ptr(src),
+                N.ptr(src_stats), src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y), N.ptr(ypool),
+                N.ptr(part), B, H, H, layer.cin, layer.cout, wp.pieces, N.stream(), tag=tag + " pool",
+                pieces=wp.pieces)
+    elif wp.pieces:
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split", *args, wp.pieces,
                 N.stream(), tag=tag, pieces=wp.pieces)
     else:
@@ -312,6 +333,8 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     st = _empty(B, layer.cout, 2, like=w)
     N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
            N.stream())
+    if pool_out:
+        return y, st, ypool
     if keep_act:
         return y, st, act
     return y, st
@@ -499,14 +522,30 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True):
     B = x.shape[0]
     saved = {}
     src, sst = x, None
-    for L in plan.enc:
+    pooled = None   # the previous layer's max-pooled raw output, when it emitted one
+    for i, L in enumerate(plan.enc):
         w, b = params[L.name + ".weight"], params[L.name + ".bias"]
         wp = _wp(packs, L.name, 0)
-        if train and L.src_mode == ACT_NORM_POOL:
+        if wp is None:
+            wp = pack_weight(w, L, dgrad=False)
+        nxt = plan.enc[i + 1] if i + 1 < len(plan.enc) else None
+        # producer of a max-pool-fed layer: emit the pooled raw output in the epilogue, so
+        # the consumer (and its wgrad) read (H/2)^2 pixels in ACT_NORM mode instead of
+        # pooling the full-resolution output while staging
+        pool_out = (nxt is not None and nxt.src_mode == ACT_NORM_POOL and L.src_mode == ACT_NORM
+                    and pool_out_ok(L, wp))
+        if pooled is not None:
+            y, st = conv_forward(pooled, sst, L, w, b, B, wp=wp, mode=ACT_NORM)
+            if train:
+                saved[L.name + ".pool_in"] = pooled
+        elif train and L.src_mode == ACT_NORM_POOL:
             y, st, act = conv_forward(src, sst, L, w, b, B, keep_act=True, wp=wp)
             saved[L.name + ".act_in"] = act
+        elif pool_out:
+            y, st, ypool = conv_forward(src, sst, L, w, b, B, wp=wp, pool_out=True)
         else:
             y, st = conv_forward(src, sst, L, w, b, B, wp=wp)
+        pooled = ypool if pool_out else None
         if train:
             saved[L.name] = (y, st)
         src, sst = y, st
@@ -543,6 +582,8 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
         mode = L.src_mode
         if i == 0:
             src, sst = x, None
+        elif L.name + ".pool_in" in saved:   # the producer's pooled raw output
+            src, sst, mode = saved[L.name + ".pool_in"], saved[plan.enc[i - 1].name][1], ACT_NORM
         elif L.src_mode == ACT_NORM_POOL:
             src, sst, mode = saved[L.name + ".act_in"], None, ACT_RAW
         else:

@@ -116,6 +116,19 @@ int ebsdvae_conv3x3_fwd_split(const float* src, const float* src_stats, int src_
                               const void* wpack, const float* bias, float* y, float* stat_part,
                               float* act_out, int B, int H, int W, int cin, int cout, int pieces,
                               ebsdvae_stream_t stream);
+/* Forward of a layer whose output the next layer max-pools (latice/model.py:111-112, 114-115,
+ * 117-118, 120-121: building_blocks then nn.MaxPool2d(2, 2)): as ebsdvae_conv3x3_fwd_split
+ * (src_mode ACT_NORM) and also writes ypool = the 2x2 max of the raw output y, (B, H/2, W/2,
+ * cout) NHWC.  Because InstanceNorm's scale is positive and LeakyReLU is increasing,
+ * maxpool(lrelu(IN(y))) == lrelu(IN(ypool)) exactly, so the next conv reads ypool in ACT_NORM
+ * mode with y's statistics instead of pooling y itself.  The statistics partials group pixels
+ * differently from ebsdvae_conv3x3_fwd_split (row pairs), so they can differ in the last bits.
+ * ebsdvae_conv3x3_split_pool_ok: 1 if the shape is supported. */
+int ebsdvae_conv3x3_split_pool_ok(int H, int W, int cin, int cout, int pieces);
+int ebsdvae_conv3x3_fwd_split_pooled(const float* src, const float* src_stats, int src_mode,
+                                     const void* wpack, const float* bias, float* y, float* ypool,
+                                     float* stat_part, int B, int H, int W, int cin, int cout,
+                                     int pieces, ebsdvae_stream_t stream);
 int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpack, float* gin,
                                       const float* y_prev, const float* st_prev, int pmode,
                                       double* part, int B, int H, int W, int cin, int cout,

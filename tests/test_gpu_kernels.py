@@ -554,3 +554,29 @@ def test_conv_wgrad_split_bf16(cuda, cin, cout, H, mode, kind, prec):
         rw = rw.transpose(1, 0, 2, 3)[:, :, ::-1, ::-1]
     assert O.rel_err(host(dw), rw) < SPLIT_TOL[prec] * 2
     assert O.rel_err(host(db), rb) < 5e-5
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("cin,cout,H", [(32, 32, 128), (32, 64, 64), (64, 64, 64), (64, 128, 32),
+                                        (128, 128, 32), (128, 128, 16)])
+def test_conv3x3_split_pooled_output(cuda, cin, cout, H, prec):
+    """ebsdvae_conv3x3_fwd_split_pooled (producer of a max-pooled layer): y is bit-identical
+    to the plain split forward, ypool is exactly the 2x2 max of y, and the InstanceNorm
+    statistics (grouped by row pairs) agree to rounding."""
+    rng = np.random.default_rng(83 + cin + cout + H)
+    B = 2
+    s, mean, rstd, st = make_src(rng, B, H, cin, E.ACT_NORM)
+    w = rng.standard_normal((cout, cin, 3, 3)) * 0.05
+    b = rng.standard_normal(cout) * 0.1
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, E.ACT_NORM, E.P_POOL)
+    with E.precision(prec):
+        wp = E.pack_weight(dev(w), layer, dgrad=False)
+        if not E.pool_out_ok(layer, wp):
+            pytest.skip("pooled epilogue needs the pipelined split kernel")
+        y1, st1 = E.conv_forward(dev(s), dev(st), layer, dev(w), dev(b), B, wp=wp)
+        y2, st2, yp = E.conv_forward(dev(s), dev(st), layer, dev(w), dev(b), B, wp=wp, pool_out=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    ref_pool = torch.nn.functional.max_pool2d(y1.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    assert torch.equal(yp, ref_pool.contiguous())
+    assert O.rel_err(host(st2), host(st1)) < 1e-5

@@ -28,6 +28,10 @@ CASES = {
     "fwd128s16": ("fwd", 16, 128, 128, ACT_NORM),
     "fwd32to64p": ("fwd", 64, 32, 64, ACT_NORM_POOL),
     "fwd64to32u": ("fwd", 128, 64, 32, ACT_NORM_UP),
+    "fwd32pool": ("fwdpool", 128, 32, 32, ACT_NORM),
+    "fwd64pool": ("fwdpool", 64, 64, 64, ACT_NORM),
+    "fwd128pool": ("fwdpool", 32, 128, 128, ACT_NORM),
+    "fwd32to64n": ("fwd", 64, 32, 64, ACT_NORM),
     "dgrad32": ("dgrad", 128, 32, 32, P_ID),
     "dgrad64": ("dgrad", 64, 64, 64, P_ID),
     "dgrad32u": ("dgrad", 128, 32, 32, P_UP),
@@ -46,7 +50,7 @@ def run(name, reps, pieces, B, warm=1.0):
     flops = 2.0 * B * H * H * cin * cout * 9
     w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) * 0.05
     bias = torch.zeros(cout, device=dev)
-    if kind == "fwd":
+    if kind in ("fwd", "fwdpool"):
         Hs = 2 * H if mode == ACT_NORM_POOL else (H // 2 if mode == ACT_NORM_UP else H)
         src = torch.randn(B, Hs, Hs, cin, device=dev, generator=g)
         st = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
@@ -57,7 +61,14 @@ def run(name, reps, pieces, B, warm=1.0):
         T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, H, cout)
         part = torch.empty(B, T, cout, 2, device=dev)
 
+        yp = torch.empty(B, H // 2, H // 2, cout, device=dev)
+
         def launch():
+            if kind == "fwdpool":
+                N.call("ebsdvae_conv3x3_fwd_split_pooled", src.data_ptr(), st.data_ptr(), mode,
+                       wp.data_ptr(), bias.data_ptr(), y.data_ptr(), yp.data_ptr(), part.data_ptr(),
+                       B, H, H, cin, cout, pieces, s)
+                return
             N.call("ebsdvae_conv3x3_fwd_split", src.data_ptr(), st.data_ptr(), mode, wp.data_ptr(),
                    bias.data_ptr(), y.data_ptr(), part.data_ptr(), None, B, H, H, cin, cout, pieces, s)
     elif kind == "dgrad":
