@@ -29,9 +29,22 @@ struct WgGeom {
   int TH, TW, NI, ntx, nty, tiles, slices, tps, lTW, ltpx;
 };
 
+// tile width of the split kernels' 32-channel layers: 16 (4x16 tiles, 108 halo pixels per
+// 64) stages 20 % fewer activation pixels than 2x32 (136) and measured 4-5 % faster on the
+// 128x128 layers (tools/conv_micro.py wgrad32, wgrad32u); EBSDVAE_WG_TW=32|8 for A/B timing
+static int wg_tw_pref() {
+  static const int v = [] {
+    const char* e = getenv("EBSDVAE_WG_TW");
+    const int t = e ? atoi(e) : 16;
+    return (t == 8 || t == 32) ? t : 16;
+  }();
+  return v;
+}
+
 // pt = pixels per tile (128 for fp32, 64 for the split-bf16 kernels)
 static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g, int pt = WG_PT) {
-  g->TW = W < 32 ? W : 32;
+  const int twmax = pt == 64 && cout == 32 ? wg_tw_pref() : 32;
+  g->TW = W < twmax ? W : twmax;
   if (H * g->TW >= pt) {
     g->TH = pt / g->TW;
     g->NI = 1;
@@ -474,7 +487,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
   if (t_beg < t_end) issue(t_beg);
   for (int t = t_beg; t < t_end; ++t) {
     __syncthreads();
+#ifndef EV_WG_NOSTORE   // timing experiment only: no staging (and so no loads; wrong results)
     store();
+#endif
     __syncthreads();
     if (t + 1 < t_end) issue(t + 1);
 #pragma unroll
