@@ -185,7 +185,8 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
     }
   } else {
     const int p0 = tile * rows * W, p1 = p0 + rows * W;
-#pragma unroll 4
+    constexpr int UNR = APPLY ? 8 : 4;   // loads in flight per thread (the apply streams 3 tensors)
+#pragma unroll UNR
     for (int p = p0 + pr; p < p1; p += NPR) {
       float4 g4;
       if (pmode == P_ID) {
@@ -277,6 +278,7 @@ __global__ __launch_bounds__(256) void in_bwd_finalize_kernel(const double2* __r
 // Partials are per (b, tile) "slice" in the [slice][tap][co][ci] layout of
 // ebsdvae_wgrad_reduce.
 enum EdgeFuse : int { FUSE_FINAL = 1, FUSE_FIRST = 2 };
+constexpr int EDGE_NB_ITEMS = 8;   // staged neighbour-source items per thread (<= 2048 per band)
 
 EV_DEVINL void wave_fold8(float& v) {  // sum over the 8 pixel rows of a wave (lanes l, l^8, ...)
   v += __shfl_xor(v, 8, 64);
@@ -327,18 +329,61 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
   const float* src1 = ((FUSE == FUSE_FINAL) ? gsrc : x) + (size_t)b * H * W;
   extern __shared__ float nbs[];   // (rows + 2) x (W + 2)
   const int r0 = tile * rows, WP = W + 2;
-  for (int i = tid; i < (rows + 2) * WP; i += 256) {
-    const int r = i / WP, cc = i - r * WP;
-    const int gh = r0 - 1 + r, gw = cc - 1;
-    nbs[i] = (gh >= 0 && gh < H && gw >= 0 && gw < W) ? src1[gh * W + gw] : 0.f;
+  {
+    // all of this thread's loads in flight at once, then the LDS writes (host: <= 8 each)
+    const int nbn = (rows + 2) * WP;
+    float nv[EDGE_NB_ITEMS];
+#pragma unroll
+    for (int k = 0; k < EDGE_NB_ITEMS; ++k) {
+      const int i = tid + 256 * k;
+      const int r = i / WP, cc = i - r * WP;
+      const int gh = r0 - 1 + r, gw = cc - 1;
+      nv[k] = (i < nbn && gh >= 0 && gh < H && gw >= 0 && gw < W) ? src1[gh * W + gw] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < EDGE_NB_ITEMS; ++k)
+      if (tid + 256 * k < nbn) nbs[tid + 256 * k] = nv[k];
   }
   __syncthreads();
   const int p0 = tile * rows * W, p1 = p0 + rows * W;
-  // the FINAL reduce pass is VALU-heavy (9-tap recompute + 36 weight-gradient FMAs per
-  // pixel): 2 pixels in flight per thread; the others stream and keep 4
-  constexpr int UNR = (FUSE == FUSE_FINAL && !APPLY) ? 2 : 4;
-#pragma unroll UNR
-  for (int p = p0 + pr; p < p1; p += NPR) {
+  // software-pipelined over groups of U pixels per thread: the next group's y (and, FIRST,
+  // gnext) loads are issued before this group is processed
+  // the FINAL reduce is VALU-heavy (9-tap recompute + 36 weight-gradient FMAs per pixel)
+  // and register-bound: 2 pixels per group, loaded at the group's start, no prefetch
+  constexpr bool PF = !(FUSE == FUSE_FINAL && !APPLY);
+  constexpr int U = PF ? 4 : 2;
+  constexpr bool LG = FUSE == FUSE_FIRST;
+  auto ldy = [&](int p) {
+    return p < p1 ? ld4(yb + (size_t)p * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto ldg = [&](int p) {
+    return (LG && p < p1) ? ld4(gsrc + ((size_t)b * H * W + p) * C + c)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  float4 ycur[U], gcur[U];
+  if (PF) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ycur[u] = ldy(p0 + pr + u * NPR);
+      gcur[u] = ldg(p0 + pr + u * NPR);
+    }
+  }
+  for (int pg = p0 + pr; pg < p1; pg += U * NPR) {
+    float4 ynxt[U], gnxt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (PF) {
+        ynxt[u] = ldy(pg + (U + u) * NPR);
+        gnxt[u] = ldg(pg + (U + u) * NPR);
+      } else {
+        ycur[u] = ldy(pg + u * NPR);
+        gcur[u] = ldg(pg + u * NPR);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const int p = pg + u * NPR;
+    if (p >= p1) break;
     const int h = p / W, w = p - h * W;
     float nb[9];   // FINAL: g1[q - d(tap)] ; FIRST: x[p + d(tap)]
 #pragma unroll
@@ -359,10 +404,10 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       }
       if (!APPLY && cg == 0) bacc[0] += nb[4];   // g1[p] itself (centre tap): db14
     } else {
-      const float4 g4 = ld4(gsrc + ((size_t)b * H * W + p) * C + c);
+      const float4 g4 = gcur[u];
       ga[0] = g4.x; ga[1] = g4.y; ga[2] = g4.z; ga[3] = g4.w;
     }
-    const float4 y4 = ld4(yb + (size_t)p * C + c);
+    const float4 y4 = ycur[u];
     const float yy[4] = {y4.x, y4.y, y4.z, y4.w};
     float o[4];
 #pragma unroll
@@ -388,6 +433,11 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     }
     if (APPLY && FUSE == FUSE_FINAL)
       st4(gy + ((size_t)b * H * W + p) * C + c, make_float4(o[0], o[1], o[2], o[3]));
+    }
+    if (PF) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) { ycur[u] = ynxt[u]; gcur[u] = gnxt[u]; }
+    }
   }
   const int slice = b * T + tile;
   if (!APPLY) {   // InstanceNorm-backward plane partials (double, fixed order)
@@ -454,6 +504,7 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
 
 // dynamic LDS of in_bwd_edge_kernel: the 1-channel source of one row band + halo
 static size_t edge_lds(int H, int W, int T) { return (size_t)(H / T + 2) * (W + 2) * sizeof(float); }
+static bool edge_ok(int H, int W, int T) { return (H / T + 2) * (W + 2) <= 256 * EDGE_NB_ITEMS; }
 
 static int grid_for(size_t n4) {
   size_t g = (n4 + 255) / 256;
@@ -546,6 +597,7 @@ extern "C" int ebsdvae_in_bwd_final_reduce(const float* g1, const float* w14, co
   EV_REQUIRE(g1 && w14 && y && stats && part && wpart && bpart && C == 32,
              "in_bwd_final_reduce: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, false>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)nullptr,
                      (const float*)nullptr, (double2*)part, wpart, bpart, (float*)nullptr, H, W, T);
@@ -558,6 +610,7 @@ extern "C" int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, con
   EV_REQUIRE(g1 && w14 && y && stats && bstats && gy && C == 32,
              "in_bwd_final_apply: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)bstats,
                      (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
@@ -572,6 +625,7 @@ extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float*
   EV_REQUIRE(gnext && y && stats && bstats && x && wpart && bpart && C == 32,
              "in_bwd_first_apply_wgrad: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, gnext, (const float*)nullptr, y, (const float2*)stats,
                      (const float2*)bstats, x, (double2*)nullptr, wpart, bpart, (float*)nullptr, H, W,
