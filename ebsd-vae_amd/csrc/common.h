@@ -34,7 +34,7 @@ EV_DEVINL float lrelu(float v) { return fmaxf(v, kSlope * v); }
 EV_DEVINL float normact(float v, float2 st) { return lrelu((v - st.x) * st.y); }
 
 // how a block's output reaches its consumer (InstanceNorm backward routing)
-enum PMode : int { P_ID = 0, P_POOL = 1, P_UP = 2 };
+enum PMode : int { P_ID = 0, P_POOL = 1, P_UP = 2, P_UPSUM = 3 /* dgrad_inbwd_split only */ };
 // d lrelu / d xhat
 EV_DEVINL float slope(float xh) { return xh > 0.f ? 1.f : kSlope; }
 

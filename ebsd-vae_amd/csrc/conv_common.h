@@ -20,6 +20,11 @@ constexpr int FP_NONE = -1;   // no fused InstanceNorm-backward reduce
 // forward of a layer whose output the next layer max-pools (pipelined split kernel only):
 // the epilogue also writes the 2x2 max of the raw output y at (H/2, W/2)
 constexpr int FP_POOLOUT = 3;
+// input gradient whose consumer upsampled its source (pmode P_UPSUM at the ABI): the
+// epilogue writes the 2x2 window sums (the gradient w.r.t. the pre-upsample activation, at
+// (H/2, W/2)) instead of the full-resolution gradient, and fuses the previous block's
+// InstanceNorm-backward reduce per window
+constexpr int FP_UPSUM = 4;
 
 // Fused InstanceNorm-backward reduce of the PREVIOUS block (input-gradient convs only):
 // this conv's output is g = d loss / d a_prev (a_prev = [pool|up](lrelu(IN(y_prev))) at

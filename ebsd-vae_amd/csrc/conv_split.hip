@@ -321,9 +321,52 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         const float v = acc[mf][nf][r] + bb;
         acc[mf][nf][r] = v;
         s += v;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
-                                              vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
+        if (FP != FP_UPSUM)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
+                                                vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
       }
+    if (FP == FP_UPSUM) {
+      // y is (B, H/2, W/2, NT): the 2x2 sums of this conv's output (the upsample adjoint),
+      // and the previous block (at H/2) is reduced once per window:
+      // sum_window(g) * lrelu'(xhat) == sum_window(g * lrelu'(xhat)), xhat constant on it
+      static_assert(MF == 2, "row-pair fragments");
+      const int W2 = W >> 1;
+      const auto rq = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(y + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
+      const auto rp = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(yprev + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
+      const float2 sp = stprev[(size_t)b0 * NT + co];
+      float gs[8], v[8];
+      int off[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        int prow, pc;
+        if (W >= 32) {   // fragment 0 = row 2rp, fragment 1 = row 2rp + 1, same 32 columns
+          const int r = 2 * k;
+          gs[k] = (acc[0][nf][r] + acc[0][nf][r + 1]) + (acc[1][nf][r] + acc[1][nf][r + 1]);
+          prow = wpx0 / W >> 1;
+          pc = ((wpx0 % W + 4 * hk) >> 1) + (((r & 3) + 8 * (r >> 2)) >> 1);
+        } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
+          const int mf = k >> 2, r = 2 * (k & 3);
+          gs[k] = (acc[mf][nf][r] + acc[mf][nf][r + 1]) + (acc[mf][nf][r + 8] + acc[mf][nf][r + 9]);
+          prow = (wpx0 + mf * mfs) / W >> 1;
+          pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
+        }
+        off[k] = ((prow * W2 + pc) * NT + co) * 4;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, 0));
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, gs[k]), rq, off[k], 0, 0);
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) inbwd_acc<P_ID>(gs[k], &v[k], sp, s1, s2);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (hk == 0) ipart[((size_t)b0 * T + slot) * NT + co] = make_double2((double)s1, (double)s2);
+    }
     if (FP == FP_POOLOUT) {
       // max(lrelu(IN(y))) over a window == lrelu(IN(max y)) (IN's scale is positive, both maps
       // are monotone), so the consumer reads this tensor in ACT_NORM mode with y's statistics
@@ -356,7 +399,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         }
       }
     }
-    if (FP != FP_NONE && FP != FP_POOLOUT) {
+    if (FP != FP_NONE && FP != FP_POOLOUT && FP != FP_UPSUM) {
       constexpr int NL = FP == P_POOL ? 4 : 1;
       constexpr int GM = NF == 1 ? 32 : EV_PIPE_EPI_G;   // loads in flight per batch
       constexpr int G = (GM / NL) < MF * 16 ? (GM / NL) : MF * 16;
@@ -466,7 +509,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   // same 32 columns) so every 2x2 pooling window is lane-local; otherwise one contiguous run
   // (for W == 16 the window is already inside a fragment)
   int fpx0 = wm * MW, mfs = 32;
-  if (FP == FP_POOLOUT && W >= 32) {
+  if ((FP == FP_POOLOUT || FP == FP_UPSUM) && W >= 32) {
     const int cbs = W >> 5, rp = wm / cbs;
     fpx0 = 2 * rp * W + (wm - rp * cbs) * 32;
     mfs = W;
@@ -920,6 +963,10 @@ static void launch_x3(const X3Cfg& c, const float* src, const float* st, int mod
     switch (pmode) {
       case P_ID: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_ID, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
       case P_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_POOL, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+      case P_UPSUM:
+        if constexpr (NI == 1)
+          launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_UPSUM, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f);
+        break;
       default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_UP, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
     }
     return;
@@ -1057,7 +1104,9 @@ extern "C" int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpa
                                                  ebsdvae_stream_t stream) {
   X3Cfg c;
   EV_REQUIRE(g && wpack && gin && B > 0, "conv3x3_dgrad_inbwd_split: null pointer or empty batch");
-  EV_REQUIRE(pmode >= -1 && pmode <= P_UP, "conv3x3_dgrad_inbwd_split: bad pmode %d", pmode);
+  EV_REQUIRE(pmode >= -1 && pmode <= P_UPSUM, "conv3x3_dgrad_inbwd_split: bad pmode %d", pmode);
+  EV_REQUIRE(pmode != P_UPSUM || ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, pieces),
+             "conv3x3_dgrad_inbwd_split: summed upsample adjoint unsupported for H=%d W=%d", H, W);
   EV_REQUIRE(pmode < 0 || (y_prev && st_prev && part && (W & (W - 1)) == 0),
              "conv3x3_dgrad_inbwd_split: fused reduce needs y_prev, st_prev, part and W = 2^k");
   EV_REQUIRE(plan_split(H, W, cin, cout, pieces, &c),

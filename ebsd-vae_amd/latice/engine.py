@@ -29,6 +29,7 @@ from . import _native as N
 
 ACT_RAW, ACT_NORM, ACT_NORM_POOL, ACT_UP, ACT_NORM_UP = range(5)
 P_ID, P_POOL, P_UP = range(3)
+P_UPSUM = 3   # ebsdvae_conv3x3_dgrad_inbwd_split: P_UP with the 2x2-summed gradient as output
 KIND_CONV, KIND_CONVT = 0, 1
 
 
@@ -469,14 +470,23 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
     _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
 
 
-def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None):
+def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
     """Input gradient of `layer`.  prev = (y_prev, st_prev, pmode_prev) of the block feeding
     it: the previous block's InstanceNorm-backward reduce is then fused into the epilogue and
-    (gin, part) is returned for in_backward(..., part=part)."""
+    (gin, part) is returned for in_backward(..., part=part).
+    sum_up (pmode_prev == P_UP): where the split kernel supports it, gin is returned already
+    2x2-summed, i.e. at the previous block's resolution (then in_backward takes it as P_ID)."""
     B, H, W, _ = gy.shape
     if wd is None:
         wd = pack_weight(w, layer, dgrad=True)
-    gin = _empty(B, H, W, layer.cin, like=gy)
+    if (sum_up and prev is not None and prev[2] == P_UP and wd.pieces
+            and os.environ.get("EBSDVAE_UPSUM", "1") != "0"
+            and N.call("ebsdvae_conv3x3_split_pool_ok", H, W, layer.cout, layer.cin, wd.pieces)):
+        prev = (prev[0], prev[1], P_UPSUM)
+    if prev is not None and prev[2] == P_UPSUM:
+        gin = _empty(B, H // 2, W // 2, layer.cin, like=gy)
+    else:
+        gin = _empty(B, H, W, layer.cin, like=gy)
     tag = f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}"
     flops = conv_flops(B, H, W, layer.cin, layer.cout)
     if prev is None:
@@ -695,7 +705,11 @@ def _decoder_backward(plan, g_xhat, saved, params, grads, packs):
     for i in reversed(range(len(plan.dec))):
         L = plan.dec[i]
         y, st = saved[L.name]
-        gy = gy_last if i == len(plan.dec) - 1 else in_backward(g_next, L.pmode, y, st, part=part)
+        if i == len(plan.dec) - 1:
+            gy = gy_last
+        else:   # a summed upsample adjoint (conv_dgrad sum_up) arrives at y's resolution
+            pm = P_ID if (L.pmode == P_UP and g_next.shape[1] == y.shape[1]) else L.pmode
+            gy = in_backward(g_next, pm, y, st, part=part)
         wn, bn = L.name + ".weight", L.name + ".bias"
         src, sst = (saved["__dec_in__"], None) if i == 0 else saved[plan.dec[i - 1].name]
         dw = _grad_buf(grads, wn, params[wn])
@@ -705,7 +719,7 @@ def _decoder_backward(plan, g_xhat, saved, params, grads, packs):
         if i > 0:
             P = plan.dec[i - 1]
             g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode),
-                                      wd=_wp(packs, L.name, 1))
+                                      wd=_wp(packs, L.name, 1), sum_up=True)
         else:
             g_next = conv_dgrad(gy, L, params[wn], wd=_wp(packs, L.name, 1))
     s, C = plan.enc_side, plan.enc_channels

@@ -129,6 +129,11 @@ int ebsdvae_conv3x3_fwd_split_pooled(const float* src, const float* src_stats, i
                                      const void* wpack, const float* bias, float* y, float* ypool,
                                      float* stat_part, int B, int H, int W, int cin, int cout,
                                      int pieces, ebsdvae_stream_t stream);
+/* pmode 3 (P_UPSUM) in ebsdvae_conv3x3_dgrad_inbwd_split: as P_UP (the block feeding this
+ * conv was nearest-upsampled, latice/model.py:134-146), but gin receives the 2x2 window sums
+ * of the input gradient, (B, H/2, W/2, cout) -- the gradient w.r.t. the pre-upsample
+ * activation -- and ebsdvae_in_bwd_apply then takes it with pmode 0.  Shapes:
+ * ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, pieces). */
 int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpack, float* gin,
                                       const float* y_prev, const float* st_prev, int pmode,
                                       double* part, int B, int H, int W, int cin, int cout,

@@ -580,3 +580,37 @@ def test_conv3x3_split_pooled_output(cuda, cin, cout, H, prec):
     ref_pool = torch.nn.functional.max_pool2d(y1.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
     assert torch.equal(yp, ref_pool.contiguous())
     assert O.rel_err(host(st2), host(st1)) < 1e-5
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("cin,cout,H", [(32, 32, 128), (64, 32, 64), (128, 64, 32), (128, 128, 16)])
+def test_dgrad_summed_upsample_adjoint(cuda, cin, cout, H, prec):
+    """pmode P_UPSUM (decoder blocks feeding an upsampling consumer): the input gradient
+    comes back already 2x2-summed at the previous block's resolution, with that block's
+    InstanceNorm-backward reduce fused per window; the block gradient matches the oracle
+    and the P_UP path."""
+    rng = np.random.default_rng(97 + cin + cout + H)
+    B = 2
+    y = rng.standard_normal((B, H // 2, H // 2, cin)) * 2 + 0.5
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    gy = rng.standard_normal((B, H, H, cout))
+    wsrc = rng.standard_normal((cout, cin, 3, 3)) * 0.1
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, E.ACT_RAW, 0)
+    with E.precision(prec):
+        wd = E.pack_weight(dev(wsrc), layer, dgrad=True)
+        if not N.call("ebsdvae_conv3x3_split_pool_ok", H, H, cout, cin, wd.pieces):
+            pytest.skip("window epilogues need the pipelined split kernel")
+        y_d, st_d = dev(y), dev(st)
+        gsum, part = E.conv_dgrad(dev(gy), layer, dev(wsrc), prev=(y_d, st_d, E.P_UP), wd=wd,
+                                  sum_up=True)
+        assert gsum.shape == (B, H // 2, H // 2, cin)
+        g_prev = E.in_backward(gsum, E.P_ID, y_d, st_d, part=part)
+        gin, part2 = E.conv_dgrad(dev(gy), layer, dev(wsrc), prev=(y_d, st_d, E.P_UP), wd=wd)
+        g_prev2 = E.in_backward(gin, E.P_UP, y_d, st_d, part=part2)
+    gn = O.conv3x3_dgrad(gy, wsrc)
+    ga = O.upsample2_bwd(gn)
+    assert O.rel_err(host(gsum), ga) < SPLIT_TOL[prec]
+    ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
+    assert O.rel_err(host(g_prev), ref) < 2e-4
+    assert O.rel_err(host(g_prev), host(g_prev2)) < 2e-4
