@@ -12,6 +12,8 @@
 #include <stdint.h>
 
 #define EV_DEVINL __device__ __forceinline__
+// device lambdas that must inline (a call spills the whole register state)
+#define EV_LAMBDA_INLINE __attribute__((always_inline))
 
 namespace ev {
 

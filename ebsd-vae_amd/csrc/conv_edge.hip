@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256) void conv_cout1_rows_kernel(
   // previous row's reads of P and A
   float* P = smem;                    // [9][W + 2] per-tap partial sums
   float* A = smem + 9 * WP;           // [W][ROWS_PS] staged activation row
+
   const int nb = H / ROWS_TH;
   const int b = blockIdx.x / nb, h0 = (blockIdx.x - b * nb) * ROWS_TH;
   if (x < 18) P[(x / 2) * WP + (x & 1) * (W + 1)] = 0.f;
@@ -105,31 +106,29 @@ __global__ __launch_bounds__(256) void conv_cout1_rows_kernel(
     for (int i = 0; i < 4; ++i) fs[i] = norm_fs(sstats[(size_t)b * C + cq * 4 + i]);
   }
   const float* sb = src + (size_t)b * H * W * C;
-  // two rows in flight: r+1 and r+2 are loading while row r is computed
-  float4 nx1[C / 4], nx2[C / 4];
-  auto load_row = [&](int r, float4 (&d)[C / 4]) {
+  // three row buffers in rotation (the loop is unrolled by 3, so no register copies): while
+  // row r is computed, rows r+1 and r+2 are loading.  Loads are unconditional (row index
+  // clamped into the image; rows outside it are zeroed when staged), so the compiler's
+  // waits stay counted instead of draining every load at each row.
+  float4 bA[C / 4], bB[C / 4], bC[C / 4];
+  auto load_row = [&](int r, float4 (&d)[C / 4]) EV_LAMBDA_INLINE {
+    const int rc = min(max(r, 0), H - 1);
 #pragma unroll
-    for (int k = 0; k < C / 4; ++k)
-      d[k] = (r >= 0 && r < H) ? ld4(sb + (size_t)r * W * C + (size_t)(x + k * W) * 4)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < C / 4; ++k) d[k] = ld4(sb + (size_t)rc * W * C + (size_t)(x + k * W) * 4);
   };
   const float bb = bias ? bias[0] : 0.f;
   float acc_m = 0.f, acc_0 = 0.f;   // output rows r-1 and r (row r+1 starts from zero)
-  load_row(h0 - 1, nx1);
-  load_row(h0, nx2);
-  for (int r = h0 - 1; r <= h0 + ROWS_TH; ++r) {
+  auto step = [&](int r, float4 (&cur)[C / 4], float4 (&nxt)[C / 4]) EV_LAMBDA_INLINE {
+    load_row(r + 2, nxt);
     float* ab = A;
     const bool inside = r >= 0 && r < H;
-    float4 cur[C / 4];
-#pragma unroll
-    for (int k = 0; k < C / 4; ++k) { cur[k] = nx1[k]; nx1[k] = nx2[k]; }
-    if (r + 2 <= h0 + ROWS_TH) load_row(r + 2, nx2);
 #pragma unroll
     for (int k = 0; k < C / 4; ++k) {
       float4 v = cur[k];
-      if (NORM && inside)
+      if (NORM)
         v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]), normact_fs(v.z, fs[2]),
                         normact_fs(v.w, fs[3]));
+      if (!inside) v = make_float4(0.f, 0.f, 0.f, 0.f);
       const int e = x + k * W;
       st4(ab + (e >> 3) * ROWS_PS + cq * 4, v);
     }
@@ -163,6 +162,14 @@ __global__ __launch_bounds__(256) void conv_cout1_rows_kernel(
     if (r - 1 >= h0 && r - 1 < h0 + ROWS_TH) out[((size_t)b * H + r - 1) * W + x] = fin + bb;
     acc_m = acc_0 + cpart[1];
     acc_0 = cpart[0];
+  };
+  load_row(h0 - 1, bA);
+  load_row(h0, bB);
+  static_assert((ROWS_TH + 2) % 3 == 0, "rows per band + halo: whole groups of three");
+  for (int r = h0 - 1; r <= h0 + ROWS_TH; r += 3) {
+    step(r, bA, bC);
+    step(r + 1, bB, bA);
+    step(r + 2, bC, bB);
   }
 }
 

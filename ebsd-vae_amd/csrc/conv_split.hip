@@ -37,8 +37,6 @@ __device__ unsigned long long ev_pipe_trace[4096 * 8 * 6];
 #define EV_TACC(acc, t0)
 #endif
 
-// lambdas of the pipelined kernel must inline (a call spills the whole register state)
-#define EV_LAMBDA_INLINE __attribute__((always_inline))
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

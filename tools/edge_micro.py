@@ -60,6 +60,10 @@ def main():
         "first_apply": (lambda: N.call("ebsdvae_in_bwd_first_apply_wgrad", N.ptr(y2), N.ptr(y), N.ptr(st),
                                        N.ptr(bst), N.ptr(x), N.ptr(wpart), N.ptr(bpart), B, H, H, C, s),
                         2 * E4 + E4 // 32),
+        # references: torch's own streaming kernels on the same tensors
+        "ref_fill": (lambda: yc.fill_(1.0), E4),
+        "ref_copy": (lambda: yc.copy_(y), 2 * E4),
+        "ref_sum": (lambda: torch.sum(y, dim=(1, 2)), E4),
         "in_apply": (lambda: N.call("ebsdvae_in_bwd_apply", N.ptr(y2), P_ID, N.ptr(y), N.ptr(st),
                                     N.ptr(bst), N.ptr(gy), B, H, H, C, s), 3 * E4),
     }
