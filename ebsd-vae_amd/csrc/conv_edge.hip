@@ -133,21 +133,23 @@ __global__ __launch_bounds__(256) void conv_cout1_rows_kernel(
       st4(ab + (e >> 3) * ROWS_PS + cq * 4, v);
     }
     __syncthreads();
-    float a[C];
-#pragma unroll
-    for (int q = 0; q < C / 4; ++q) {
-      const float4 v = ld4(ab + x * ROWS_PS + q * 4);
-      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-    }
     float* pb = P;
-    // channel-major so each channel's 9 weights are adjacent (merged wide scalar loads)
+    // channel-major so each channel's 9 weights are adjacent (merged wide scalar loads); in
+    // chunks of 8 channels (72 weights) so a chunk's weights stay in SGPRs -- all 288 at once
+    // overflow them and every FMA then pays a v_readlane
     float p[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) p[t] = 0.f;
+#pragma unroll 1
+    for (int c0 = 0; c0 < C; c0 += 8) {
+      const float4 u0 = ld4(ab + x * ROWS_PS + c0), u1 = ld4(ab + x * ROWS_PS + c0 + 4);
+      const float a[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      const float* wc = w + c0 * 9;
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+      for (int c = 0; c < 8; ++c)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) p[FLIP ? 8 - t : t] = fmaf(a[c], w[c * 9 + t], p[FLIP ? 8 - t : t]);
+        for (int t = 0; t < 9; ++t) p[FLIP ? 8 - t : t] = fmaf(a[c], wc[c * 9 + t], p[FLIP ? 8 - t : t]);
+    }
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) pb[tap * WP + x + 1] = p[tap];
     __syncthreads();
