@@ -41,6 +41,19 @@ static int wg_tw_pref() {
   return v;
 }
 
+// target block count of a weight-gradient launch (slices x co tiles x ci tiles).  Every
+// slice writes a full partial dW that the batched reduce re-reads, so fewer, longer slices
+// cut that traffic (512 measured 0.2 ms/step faster than 1024; 256 leaves half the CUs'
+// block slots empty); EBSDVAE_WG_BLOCKS overrides the split kernels' target (A/B timing)
+static int wg_block_target(int pt) {
+  static const int v = [] {
+    const char* e = getenv("EBSDVAE_WG_BLOCKS");
+    const int t = e ? atoi(e) : 512;   // 2 blocks per CU x 256 CUs: one wave of blocks
+    return (t >= 64 && t <= 8192) ? t : 512;
+  }();
+  return pt == 64 ? v : 1024;
+}
+
 // pt = pixels per tile (128 for fp32, 64 for the split-bf16 kernels)
 static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g, int pt = WG_PT) {
   const int twmax = pt == 64 && cout == 32 ? wg_tw_pref() : 32;
@@ -66,7 +79,7 @@ static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g, int pt = 
   // 8x8 maps (two-image tiles) use 32-wide co tiles: the 64-wide variant exceeds 256 VGPRs
   const int co_t = cout == 1 ? 1 : (cout == 32 || g->TW == 8 ? cout / 32 : cout / 64);
   const int ci_t = cin == 1 ? 1 : (cout == 1 ? 1 : cin / 32);
-  const int want = 1024 / (co_t * ci_t);
+  const int want = wg_block_target(pt) / (co_t * ci_t);
   int tps = 4;
   while ((g->tiles + tps - 1) / tps > (want > 1 ? want : 1)) tps *= 2;
   g->tps = tps;
