@@ -222,8 +222,8 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
     ap.add_argument("--probe-every", type=int, default=5,
                     help="bracket the conv launches with HIP events on every k-th timed step")
-    ap.add_argument("--precision", default=None, choices=["fp32", "bf16x6", "bf16x3"],
-                    help="conv arithmetic (default: the engine default, bf16x6)")
+    ap.add_argument("--precision", default=None, choices=["fp32", "bf16x6", "bf16x3", "f16x3"],
+                    help="conv arithmetic (default: the engine default, f16x3)")
     ap.add_argument("--c4-batches", type=int, default=1024,
                     help="encoder-only inference batches of 1024 for the c4 latents/s field (0: skip)")
     ap.add_argument("--c5-steps", type=int, default=10,
@@ -327,7 +327,10 @@ def main():
             "fp32": " (v_mfma_f32_32x32x2_f32)",
             "bf16x6": " (fp32 operands split into 3 bf16 pieces, 6 bf16 MFMA products per fp32"
                       " product, fp32 accumulation: fp32-grade, same parity gates as fp32)",
-            "bf16x3": " (2 bf16 pieces, 3 products: ~2^-16.5 per product)"}[E.get_precision()],
+            "bf16x3": " (2 bf16 pieces, 3 products: ~2^-16.5 per product)",
+            "f16x3": " (forward convs: fp32 operands split into 2 fp16 pieces, weights x256, 3 fp16"
+                     " MFMA products, ~2^-22.5 per product; input/weight gradients bf16x6; same"
+                     " parity gates as fp32)"}[E.get_precision()],
         "config": {"workload": f"c{2 if world == 1 else 3}: VariationalAutoEncoderRawData "
                                f"{args.image_size}x{args.image_size}, latent {args.latent_dim}, "
                                f"batch {args.batch}/GPU, fwd+loss+bwd+Adam"

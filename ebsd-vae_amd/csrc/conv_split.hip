@@ -59,16 +59,47 @@ EV_DEVINL void split_bf16(float x, __bf16 (&p)[NP]) {
   }
 }
 
+// Piece format NP_F16 ("f16x3", forward convs only): two fp16 pieces
+//     x0 = f16(x), x1 = f16(x - x0)      (11 significand bits each, |x - x0 - x1| <= 2^-23 |x|
+//                                          for normal x1, 2^-25 absolute below it)
+// and the three products a0b0 + a0b1 + a1b0 on v_mfma_f32_32x32x16_f16 (the dropped a1b1 is
+// <= 2^-24 relative): ~2^-22.5 per product, at the bf16x3 rate.  fp16's range is narrow, so
+// the weights are packed as w * kF16WScale (2^8: small weights keep x1 in the normal range;
+// |w| < 255 stays finite) and the epilogue multiplies the accumulators by the exact inverse.
+// The forward operands are normalised activations (IN + LeakyReLU, |x| <= sqrt(H*W)), which
+// fp16 holds; gradients span far smaller magnitudes, so dgrad / wgrad stay on bf16x6.
+constexpr int NP_F16 = EBSDVAE_PIECES_F16;
+constexpr float kF16WScale = 256.f;
+constexpr int npc(int np) { return np == NP_F16 ? 2 : np; }   // pieces per operand
+
 template <int NP>
-EV_DEVINL void split4(float4 v, bf16x4 (&out)[NP]) {
+EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
   const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    __bf16 p[NP];
-    split_bf16<NP>(e[c], p);
+    if constexpr (NP == NP_F16) {   // fp16 bit patterns in the 16-bit piece slots
+      const _Float16 h0 = (_Float16)e[c];
+      const _Float16 h1 = (_Float16)(e[c] - (float)h0);
+      out[0][c] = __builtin_bit_cast(__bf16, h0);
+      out[1][c] = __builtin_bit_cast(__bf16, h1);
+    } else {
+      __bf16 p[NP];
+      split_bf16<NP>(e[c], p);
 #pragma unroll
-    for (int i = 0; i < NP; ++i) out[i][c] = p[i];
+      for (int i = 0; i < NP; ++i) out[i][c] = p[i];
+    }
   }
+}
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// one 32x32x16 product of two piece fragments (bf16, or fp16 bits for NP_F16)
+template <int NP>
+EV_DEVINL f32x16 mfma_piece(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (NP == NP_F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 EV_DEVINL bf16x8 lds_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -473,7 +504,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr int WN = NWV / WM;
   constexpr int NT = WN * NF * 32;               // == Cout
   constexpr int MW = MF * 32;
-  constexpr int WSLAB = XTAPS * NP * NT * 16;
+  constexpr int NPC = npc(NP);                   // pieces per operand
+  constexpr int WSLAB = XTAPS * NPC * NT * 16;
   constexpr int WPER = pipe_dma_per(WSLAB, NWV);  // 1-KiB weight pieces per wave per chunk
   constexpr int WSLABP = WPER * NWV * 1024;       // LDS weight buffer (padded to whole rounds)
   constexpr bool POOL = (MODE == ACT_NORM_POOL);
@@ -642,11 +674,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
         st4(act_out + (((size_t)(sb0[sl] + img_w) * H + sh0[sl] + hh - 1) * W + gw) * Cin +
                 sch[sl] * XCK + q * 4, v);
     }
-    bf16x4 pc[NP];
+    bf16x4 pc[NPC];
     split4<NP>(v, pc);
     char* d = lx + ldo[k];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) *reinterpret_cast<bf16x4*>(d + 16 * i) = pc[i];
+    for (int i = 0; i < NPC; ++i) *reinterpret_cast<bf16x4*>(d + 16 * i) = pc[i];
   };
   auto stage_fs = [&](auto slot_c, float2 (&fs)[4]) EV_LAMBDA_INLINE {
     constexpr int sl = decltype(slot_c)::value;
@@ -682,6 +714,14 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     coords(it_done, b0, h0, ch);
     const int im = NI == 1 ? 0 : (wm * MW) / tpx;   // the wave's pixels lie in one image
     const int wpx0 = fpx0 - im * tpx;
+    if constexpr (NP == NP_F16) {   // undo the weight scale (exact: a power of two)
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[mf][nf][r] *= 1.f / kF16WScale;
+    }
     if (NI == 1 || b0 + im < B)
       pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
                                     (h0 * W + wm * MW - im * tpx) / MW, wn * NF * 32, hk, l32,
@@ -715,32 +755,32 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     char* lxn = lx0 + (1 - P) * xslab;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
-      bf16x8 a[NP][MF], b[NP][NF];
+      bf16x8 a[NPC][MF], b[NPC][NF];
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
         const char* pa = lx + (abase[mf] + toff[s]) * XPS;
 #pragma unroll
-        for (int i = 0; i < NP; ++i) a[i][mf] = lds_frag(pa + 16 * i);
+        for (int i = 0; i < NPC; ++i) a[i][mf] = lds_frag(pa + 16 * i);
       }
       const int t = 2 * s + hk;
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf) {
-        const char* pb = lw + ((t * NP) * NT + ncol + nf * 32) * 16;
+        const char* pb = lw + ((t * NPC) * NT + ncol + nf * 32) * 16;
 #pragma unroll
-        for (int i = 0; i < NP; ++i) b[i][nf] = lds_frag(pb + i * NT * 16);
+        for (int i = 0; i < NPC; ++i) b[i][nf] = lds_frag(pb + i * NT * 16);
       }
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf) {
-          if (NP == 3) {
+          if constexpr (NP == 3) {
             acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mf], b[NP - 2][nf], acc[mf][nf], 0, 0, 0);
             acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[NP - 1][mf], b[0][nf], acc[mf][nf], 0, 0, 0);
             acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mf], b[NP - 1][nf], acc[mf][nf], 0, 0, 0);
           }
-          acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mf], b[0][nf], acc[mf][nf], 0, 0, 0);
-          acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mf], b[1][nf], acc[mf][nf], 0, 0, 0);
-          acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mf], b[0][nf], acc[mf][nf], 0, 0, 0);
+          acc[mf][nf] = mfma_piece<NP>(a[1][mf], b[0][nf], acc[mf][nf]);
+          acc[mf][nf] = mfma_piece<NP>(a[0][mf], b[1][nf], acc[mf][nf]);
+          acc[mf][nf] = mfma_piece<NP>(a[0][mf], b[0][nf], acc[mf][nf]);
         }
 #ifdef EV_PIPE_LATE_ISSUE
       if (s == 0) {   // behind the first k-step's MFMAs, so the matrix pipe covers the issue
@@ -835,7 +875,15 @@ __global__ void pack_split_kernel(const PackBatch pb, int np) {
       else idx = ((size_t)ci * q.cout + co) * 9 + (q.for_dgrad ? t : 8 - t);
       w = q.src[idx];
     }
-    const size_t base = ((size_t)(chunk * XTAPS + t) * np) * co_ * XCK + (size_t)o * XCK + c8;
+    const size_t base = ((size_t)(chunk * XTAPS + t) * npc(np)) * co_ * XCK + (size_t)o * XCK + c8;
+    if (np == NP_F16) {   // two fp16 pieces of the scaled weight (conv3x3_pipe_kernel undoes it)
+      const float ws = w * kF16WScale;
+      const _Float16 h0 = (_Float16)ws;
+      const _Float16 h1 = (_Float16)(ws - (float)h0);
+      d[base] = __builtin_bit_cast(__bf16, h0);
+      d[base + (size_t)co_ * XCK] = __builtin_bit_cast(__bf16, h1);
+      continue;
+    }
     float rr = w;
     for (int i = 0; i < np; ++i) {
       const __bf16 p = (__bf16)rr;
@@ -887,12 +935,14 @@ struct X3Cfg {
 // NP = 2: Cout 128 -> 8 waves x M 256; Cout 64 / 32 -> 4 waves x M 256 (2 blocks / CU).
 // NP = 3: the 3-piece weight slab is 1.5x larger, so every Cout runs 8 waves (M 256 for
 // Cout 128, M 512 otherwise) with one block per CU.
+// NP_F16 (forward only, pipelined kernel only) takes the NP = 3 geometry with 2-piece slabs.
 static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
-  if ((np != 2 && np != 3) || cin % (2 * XCK) || !(cout == 128 || cout == 64 || cout == 32)) return false;
-  c->M = (np == 3 && cout != 128) ? 512 : 256;
+  if ((np != 2 && np != 3 && np != NP_F16) || cin % (2 * XCK) || !(cout == 128 || cout == 64 || cout == 32)) return false;
+  if (np == NP_F16 && !use_pipe()) return false;
+  c->M = (np != 2 && cout != 128) ? 512 : 256;
   c->NI = 1;
   c->NT = cout;
-  c->nwv = (cout == 128 || np == 3) ? 8 : 4;
+  c->nwv = (cout == 128 || np != 2) ? 8 : 4;
   if (H * W < c->M) {
     // 8x8 maps (bf16x6, 128 channels): tiles of two whole images, 128 pixels, 8 waves of
     // 64 px x 32 co; pipelined kernel only
@@ -911,11 +961,11 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   c->KX = (pixI * 2 + tpg - 1) / tpg;
   const int kxmax = np == 2 ? (cout == 128 ? 2 : (cout == 64 ? 5 : 7)) : (cout == 128 ? 2 : (cout == 64 ? 4 : 5));
   if (c->KX > kxmax) return false;
-  const int wslab = XTAPS * np * cout * 16;
+  const int wslab = XTAPS * npc(np) * cout * 16;
   c->lds = 2 * (size_t)wslab + 2 * (size_t)(pix + 1) * XPS;
   c->lds_pipe = 2 * (size_t)pipe_dma_per(wslab, c->nwv) * c->nwv * 1024 + 2 * (size_t)(pix + 1) * XPS;
   if (c->lds_pipe > 160 * 1024) c->lds_pipe = 0;
-  if (c->NI > 1) return c->lds_pipe != 0;   // no non-persistent form for multi-image tiles
+  if (c->NI > 1 || np == NP_F16) return c->lds_pipe != 0;   // pipelined kernel only
   return c->lds <= 160 * 1024;
 }
 
@@ -940,7 +990,7 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
                        f.stprev, f.part, f.ypool);
     return;
   }
-  if constexpr (NI == 1 && FP != FP_POOLOUT) {
+  if constexpr (NI == 1 && FP != FP_POOLOUT && NP != NP_F16) {
     auto k = conv3x3_split_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP>;
     static bool once = false;
     if (!once) {
@@ -957,7 +1007,9 @@ template <int NP, int NWV, int WM, int MF, int NF, int KX, int NI = 1>
 static void launch_x3(const X3Cfg& c, const float* src, const float* st, int mode, const void* wp,
                       const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                       int cin, hipStream_t s, int pmode, const InBwdFuse& f) {
-  if (pmode >= 0) {
+  if constexpr (NP == NP_F16) {
+    if (pmode >= 0) return;   // forward-only piece format (dispatch_split never gets here)
+  } else if (pmode >= 0) {
     switch (pmode) {
       case P_ID: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_ID, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
       case P_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_POOL, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
@@ -995,6 +1047,14 @@ static void dispatch_split(const X3Cfg& c, int np, const float* src, const float
       launch_x3<2, 4, 4, 2, 2, 5>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else
       launch_x3<2, 4, 4, 2, 1, 7>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+  } else if (np == NP_F16) {   // forward only (no pmode / dgrad instantiations)
+    if (pmode >= 0) return;
+    if (cout == 128)
+      launch_x3<NP_F16, 8, 4, 2, 2, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else if (cout == 64)
+      launch_x3<NP_F16, 8, 8, 2, 2, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else
+      launch_x3<NP_F16, 8, 8, 2, 1, 5>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
   } else {
     if (cout == 128 && c.NI > 1)   // two 8x8 images per tile: 2 x 4 waves of 64 px x 32 co
       launch_x3<3, 8, 2, 2, 1, 1, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
@@ -1029,13 +1089,14 @@ extern "C" int ebsdvae_conv3x3_split_stat_tiles(int H, int W, int cout) {
 }
 
 extern "C" size_t ebsdvae_pack_split_bytes(int cin, int cout, int pieces) {
-  return (size_t)(cin / XCK) * XTAPS * pieces * cout * XCK * 2;
+  return (size_t)(cin / XCK) * XTAPS * npc(pieces) * cout * XCK * 2;
 }
 
 extern "C" int ebsdvae_pack_conv_weights_split(const ebsdvae_pack_desc* descs, int n, int pieces,
                                                ebsdvae_stream_t stream) {
   EV_REQUIRE(descs && n > 0 && n <= EBSDVAE_MAX_PACK, "pack_conv_weights_split: n=%d out of range", n);
-  EV_REQUIRE(pieces == 2 || pieces == 3, "pack_conv_weights_split: pieces=%d (2 or 3)", pieces);
+  EV_REQUIRE(pieces == 2 || pieces == 3 || pieces == NP_F16,
+             "pack_conv_weights_split: pieces=%d (2, 3 or %d)", pieces, NP_F16);
   PackBatch pb;
   int maxn = 0;
   for (int i = 0; i < n; ++i) {
@@ -1102,6 +1163,7 @@ extern "C" int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpa
                                                  ebsdvae_stream_t stream) {
   X3Cfg c;
   EV_REQUIRE(g && wpack && gin && B > 0, "conv3x3_dgrad_inbwd_split: null pointer or empty batch");
+  EV_REQUIRE(pieces != NP_F16, "conv3x3_dgrad_inbwd_split: fp16 pieces are forward-only");
   EV_REQUIRE(pmode >= -1 && pmode <= P_UPSUM, "conv3x3_dgrad_inbwd_split: bad pmode %d", pmode);
   EV_REQUIRE(pmode != P_UPSUM || ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, pieces),
              "conv3x3_dgrad_inbwd_split: summed upsample adjoint unsupported for H=%d W=%d", H, W);

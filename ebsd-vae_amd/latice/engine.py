@@ -151,7 +151,7 @@ BF16_MFMA_TFLOPS = 2516.6
 def mfma_peak(pieces: int) -> float:
     """Peak in fp32-equivalent TFLOP/s of a conv launch: fp32 MFMA, or the bf16 MFMA peak
     divided by the bf16 products per fp32 product of the split (3 or 6)."""
-    return FP32_MFMA_TFLOPS if not pieces else BF16_MFMA_TFLOPS / {2: 3, 3: 6}[pieces]
+    return FP32_MFMA_TFLOPS if not pieces else BF16_MFMA_TFLOPS / {2: 3, 3: 6, PIECES_F16: 3}[pieces]
 
 
 def _launch(family, flops, fn, *args, tag=None, pieces=0):
@@ -179,12 +179,18 @@ def _empty(*shape, like):
 # Conv arithmetic (csrc/conv_fwd.hip, csrc/conv_split.hip):
 #   "fp32"   v_mfma_f32_32x32x2_f32 (exact fp32 products);
 #   "bf16x6" 3-piece split-bf16 MFMA, 6 products per fp32 product (~2^-25, fp32 grade);
-#   "bf16x3" 2-piece split-bf16 MFMA, 3 products (~2^-16.5 per product).
+#   "bf16x3" 2-piece split-bf16 MFMA, 3 products (~2^-16.5 per product);
+#   "f16x3"  forward convs on 2-piece split-fp16 MFMA (x0 = f16(x), x1 = f16(x - x0); weights
+#            packed x256), 3 products (~2^-22.5 per product); input / weight gradients on
+#            bf16x6 (gradients span magnitudes below fp16's range).
 # Split modes cover every conv layer the split kernel supports (Cout in {32,64,128},
-# H*W >= 256); the others stay fp32.
-_PIECES = {"fp32": 0, "bf16x3": 2, "bf16x6": 3}
-# default: the fp32-grade split (passes every fp32 parity gate; tests/test_gpu_model.py)
-_PRECISION = os.environ.get("EBSDVAE_PRECISION", "bf16x6")
+# H*W >= 256, plus the 8x8 maps for bf16x6); the others stay fp32.
+PIECES_F16 = 16   # EBSDVAE_PIECES_F16 (include/ebsdvae.h)
+_PIECES = {"fp32": 0, "bf16x3": 2, "bf16x6": 3, "f16x3": 3}
+_FWD_PIECES = {"f16x3": PIECES_F16}   # forward-conv piece format where it differs
+# default: f16x3 (forward) + bf16x6 (gradients); passes every fp32 parity gate
+# (tests/test_gpu_model.py runs fp32, bf16x6 and f16x3)
+_PRECISION = os.environ.get("EBSDVAE_PRECISION", "f16x3")
 if _PRECISION not in _PIECES:
     raise ValueError(f"EBSDVAE_PRECISION must be one of {sorted(_PIECES)}")
 _SPLIT_CACHE = {}
@@ -212,16 +218,23 @@ def precision(mode: str):
         set_precision(old)
 
 
-def split_pieces(H: int, cin: int, cout: int) -> int:
-    """bf16 pieces per operand of a conv with input channels cin -> cout at HxH (0 = fp32)."""
+def _supported(H: int, cin: int, cout: int, np_: int) -> bool:
+    key = (H, cin, cout, np_)
+    if key not in _SPLIT_CACHE:
+        _SPLIT_CACHE[key] = bool(N.call("ebsdvae_conv3x3_split_supported", H, H, cin, cout, np_))
+    return _SPLIT_CACHE[key]
+
+
+def split_pieces(H: int, cin: int, cout: int, dgrad: bool = False) -> int:
+    """Piece format of a conv with input channels cin -> cout at HxH: bf16 pieces per operand
+    (2 or 3), PIECES_F16, or 0 = fp32.  dgrad: the input-gradient pack (never fp16)."""
     np_ = _PIECES[_PRECISION]
     if np_ == 0:
         return 0
-    key = (H, cin, cout, np_)
-    if key not in _SPLIT_CACHE:
-        ok = N.call("ebsdvae_conv3x3_split_supported", H, H, cin, cout, np_)
-        _SPLIT_CACHE[key] = np_ if ok else 0
-    return _SPLIT_CACHE[key]
+    f16 = _FWD_PIECES.get(_PRECISION)
+    if f16 and not dgrad and _supported(H, cin, cout, f16):
+        return f16
+    return np_ if _supported(H, cin, cout, np_) else 0
 
 
 @dataclass
@@ -239,7 +252,7 @@ def _pack_numel(layer: ConvLayer, pieces: int, dgrad: bool) -> int:
 
 def pack_weight(w, layer: ConvLayer, dgrad: bool) -> PackedW:
     ci_, co_ = (layer.cout, layer.cin) if dgrad else (layer.cin, layer.cout)
-    np_ = split_pieces(layer.H, ci_, co_)
+    np_ = split_pieces(layer.H, ci_, co_, dgrad)
     out = _empty(_pack_numel(layer, np_, dgrad), like=w)
     if np_:
         d = (N.PackDesc * 1)(N.PackDesc(N.ptr(w), N.ptr(out), layer.cin, layer.cout, layer.kind, int(dgrad)))
@@ -270,7 +283,7 @@ class PackSet:
 
     def _one(self, L, w, dgrad, descs):
         ci_, co_ = (L.cout, L.cin) if dgrad else (L.cin, L.cout)
-        np_ = split_pieces(L.H, ci_, co_)
+        np_ = split_pieces(L.H, ci_, co_, dgrad)
         t = _empty(_pack_numel(L, np_, dgrad), like=w)
         descs.setdefault(np_, []).append(N.PackDesc(N.ptr(w), N.ptr(t), L.cin, L.cout, L.kind, int(dgrad)))
         return PackedW(t, np_)

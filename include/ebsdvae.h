@@ -102,11 +102,15 @@ int ebsdvae_conv3x3_cout1_dgrad(const float* g, const float* w, float* gin, int 
  * x2 = bf16(x - x0 - x1)) and every product keeps the terms of total order < pieces, on
  * v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
  *   pieces = 2 ("bf16x3", 3 MFMAs, ~2^-16.5 relative error per product);
- *   pieces = 3 ("bf16x6", 6 MFMAs, ~2^-25: fp32 grade).
+ *   pieces = 3 ("bf16x6", 6 MFMAs, ~2^-25: fp32 grade);
+ *   pieces = EBSDVAE_PIECES_F16 ("f16x3", forward only: two fp16 pieces x0 = f16(x),
+ *     x1 = f16(x - x0) on v_mfma_f32_32x32x16_f16, 3 MFMAs, ~2^-22.5 per product; the pack
+ *     holds w * 256 so small weights keep full precision, |w| < 255).
  * Weights use the split pack ([cin'/8][tap 0..9][piece][cout'][8] bf16,
  * ebsdvae_pack_split_bytes bytes).  Shapes: ebsdvae_conv3x3_split_supported; InstanceNorm
  * partials use ebsdvae_conv3x3_split_stat_tiles tiles per image.  pmode = -1 in
  * ebsdvae_conv3x3_dgrad_inbwd_split is a plain input gradient (y_prev/st_prev/part unused). */
+#define EBSDVAE_PIECES_F16 16
 int ebsdvae_conv3x3_split_supported(int H, int W, int cin, int cout, int pieces);
 int ebsdvae_conv3x3_split_stat_tiles(int H, int W, int cout);
 size_t ebsdvae_pack_split_bytes(int cin, int cout, int pieces);

@@ -440,20 +440,26 @@ def test_batched_wgrad_reduce_matches_per_layer(cuda):
         assert np.abs(host(dwb) - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
 
 
-SPLIT_TOL = {"bf16x3": 1e-4, "bf16x6": 2e-5}   # ~2^-16.5 / ~2^-25 per product
+# ~2^-16.5 / ~2^-25 / ~2^-22.5 per product
+SPLIT_TOL = {"bf16x3": 1e-4, "bf16x6": 2e-5, "f16x3": 2e-5}
+FWD_PIECES = {"bf16x3": 2, "bf16x6": 3, "f16x3": E.PIECES_F16}
 
 
-@pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("wscale", [0.1, 1e-3])
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16x6", "f16x3"])
 @pytest.mark.parametrize("cin,cout,H,mode", [c for c in FWD_CASES if c[0] > 1 and c[2] >= 8])
-def test_conv3x3_fwd_split_bf16(cuda, cin, cout, H, mode, prec):
-    """Split-bf16 forward == float64 oracle (bf16x3 within 1e-4, bf16x6 at fp32 grade)."""
-    if not N.call("ebsdvae_conv3x3_split_supported", H, H, cin, cout, {"bf16x3": 2, "bf16x6": 3}[prec]):
+def test_conv3x3_fwd_split_bf16(cuda, cin, cout, H, mode, prec, wscale):
+    """Split forward == float64 oracle (bf16x3 within 1e-4, bf16x6 and f16x3 at 2e-5).
+    wscale 1e-3: small weights, whose fp16 pieces rely on the pack's x256 scale."""
+    if wscale != 0.1 and prec != "f16x3":
+        pytest.skip("weight-scale sweep targets the fp16 pieces")
+    if not N.call("ebsdvae_conv3x3_split_supported", H, H, cin, cout, FWD_PIECES[prec]):
         pytest.skip("shape not covered by the split kernel")
     rng = np.random.default_rng(31 + cin + cout + H + mode)
     B = 2
     s, mean, rstd, st = make_src(rng, B, H, cin, mode)
-    w = rng.standard_normal((cout, cin, 3, 3)) * 0.1
-    b = rng.standard_normal(cout) * 0.1
+    w = rng.standard_normal((cout, cin, 3, 3)) * wscale
+    b = rng.standard_normal(cout) * wscale
     layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
     old = E.get_precision()
     E.set_precision(prec)

@@ -42,10 +42,10 @@ def h(t):
     return t.detach().double().cpu().numpy()
 
 
-@pytest.fixture(params=["bf16x6", "fp32"])
+@pytest.fixture(params=["bf16x6", "fp32", "f16x3"])
 def prec(request):
-    """The model-level gates hold for the default fp32-grade split-bf16 convs AND the pure
-    fp32-MFMA convs."""
+    """The model-level gates hold for the fp32-grade split-bf16 convs, the pure fp32-MFMA
+    convs AND the split-fp16 forward (f16x3; its backward is bf16x6)."""
     from latice import engine as E
     with E.precision(request.param):
         yield request.param
