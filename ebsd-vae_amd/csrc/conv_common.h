@@ -147,6 +147,8 @@ struct InBwdFuse {
   const float2* stprev = nullptr;
   double2* part = nullptr;
   float* ypool = nullptr;   // FP_POOLOUT forward: the max-pooled raw output
+  const float* gmax = nullptr;   // NP_F16 input gradient: per-tile max |g| (B, gmT)
+  int gmT = 0;
 };
 
 }  // namespace ev

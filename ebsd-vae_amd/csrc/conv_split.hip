@@ -91,6 +91,19 @@ EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
   }
 }
 
+// NP_F16 input gradient: the gradient operand of image b is scaled by 2^k, k such that
+// max|g[b]| * 2^k lies in [2^11, 2^12), from the per-tile maxima (B, gmT) that the
+// InstanceNorm-backward apply wrote (0 without them, or for a zero / non-finite maximum)
+EV_DEVINL int f16_gshift(const float* __restrict__ gmax, int gmT, int b) {
+  if (!gmax) return 0;
+  float m = 0.f;
+  for (int t = 0; t < gmT; ++t) m = fmaxf(m, gmax[(size_t)b * gmT + t]);
+  if (!(m > 0.f) || !(m <= 3.4e38f)) return 0;
+  int e;
+  (void)frexpf(m, &e);   // m = f * 2^e, f in [0.5, 1)
+  return min(max(12 - e, -100), 100);
+}
+
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 // one 32x32x16 product of two piece fragments (bf16, or fp16 bits for NP_F16)
 template <int NP>
@@ -500,7 +513,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
     float* __restrict__ act_out, int B, int H, int W, int Cin, int TH, int tpb,
     const float* __restrict__ yprev, const float2* __restrict__ stprev, double2* __restrict__ ipart,
-    float* __restrict__ ypool) {
+    float* __restrict__ ypool, const float* __restrict__ gmax, int gmT) {
   constexpr int WN = NWV / WM;
   constexpr int NT = WN * NF * 32;               // == Cout
   constexpr int MW = MF * 32;
@@ -512,6 +525,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_POOL || MODE == ACT_NORM_UP);
   constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
   constexpr int NR = POOL ? 4 : 1;
+  constexpr bool GS = (NP == NP_F16 && MODE == ACT_RAW);   // per-image gradient scale
   constexpr int PD = POOL ? 1 : 2;               // halo prefetch distance (iterations)
   static_assert(PD == 1 || KX * NR <= 7, "pipe_barrier keeps at most 7 loads in flight");
   extern __shared__ __attribute__((aligned(16))) char xsm[];
@@ -603,6 +617,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   float2 st[PD][4];
   int okm[PD];
   int sb0[PD], sh0[PD], sch[PD];   // tile image / first row / chunk of the slot's data
+  float gsc[PD];                   // GS: the slot image's gradient scale
+  int gs_b = -1;                   // GS: image whose shift gs_k holds
+  int gs_k = 0;
+  auto gshift = [&](int b) EV_LAMBDA_INLINE {
+    if (b != gs_b) { gs_b = b; gs_k = f16_gshift(gmax, gmT, b); }
+    return gs_k;
+  };
 
   auto coords = [&](int it, int& b0, int& h0, int& ch) EV_LAMBDA_INLINE {
     const int tl = it / nch;
@@ -620,6 +641,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     int b0, h0, ch;
     coords(it, b0, h0, ch);
     sb0[sl] = b0; sh0[sl] = h0; sch[sl] = ch;
+    if constexpr (GS) gsc[sl] = ldexpf(1.f, gshift(b0));
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)b0 * Hs * Ws * Cin), 0,
                                                       NI == 1 ? img_bytes : img_bytes * min(NI, B - b0),
                                                       0x00020000);
@@ -666,6 +688,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
                       normact_fs(v.w, fs[3]));
     const bool ok = (okm[sl] >> k) & 1;
     v = make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+    if constexpr (GS) v = make_float4(v.x * gsc[sl], v.y * gsc[sl], v.z * gsc[sl], v.w * gsc[sl]);
     if (act_out) {   // uniform: materialise the (pooled) activation for the wgrad
       const int pixl = (tig + WPI * 64 * k) >> 1;
       const int hh = pixl / WP, gw = pixl - hh * WP - 1;
@@ -714,13 +737,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     coords(it_done, b0, h0, ch);
     const int im = NI == 1 ? 0 : (wm * MW) / tpx;   // the wave's pixels lie in one image
     const int wpx0 = fpx0 - im * tpx;
-    if constexpr (NP == NP_F16) {   // undo the weight scale (exact: a power of two)
+    if constexpr (NP == NP_F16) {   // undo the weight [and gradient] scale (powers of two)
+      float sc = 1.f / kF16WScale;
+      if constexpr (GS) sc = ldexpf(sc, -gshift(b0 + im));
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[mf][nf][r] *= 1.f / kF16WScale;
+          for (int r = 0; r < 16; ++r) acc[mf][nf][r] *= sc;
     }
     if (NI == 1 || b0 + im < B)
       pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
@@ -987,7 +1012,7 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
     const int nblk = (ntiles + tpb - 1) / tpb;
     hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), c.lds_pipe, s, src, (const float2*)st,
                        (const char*)wp, bias, y, (float2*)part, aout, B, H, W, cin, c.TH, tpb, f.yprev,
-                       f.stprev, f.part, f.ypool);
+                       f.stprev, f.part, f.ypool, f.gmax, f.gmT);
     return;
   }
   if constexpr (NI == 1 && FP != FP_POOLOUT && NP != NP_F16) {
@@ -1007,9 +1032,7 @@ template <int NP, int NWV, int WM, int MF, int NF, int KX, int NI = 1>
 static void launch_x3(const X3Cfg& c, const float* src, const float* st, int mode, const void* wp,
                       const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                       int cin, hipStream_t s, int pmode, const InBwdFuse& f) {
-  if constexpr (NP == NP_F16) {
-    if (pmode >= 0) return;   // forward-only piece format (dispatch_split never gets here)
-  } else if (pmode >= 0) {
+  if (pmode >= 0) {
     switch (pmode) {
       case P_ID: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_ID, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
       case P_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_POOL, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
@@ -1047,8 +1070,7 @@ static void dispatch_split(const X3Cfg& c, int np, const float* src, const float
       launch_x3<2, 4, 4, 2, 2, 5>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else
       launch_x3<2, 4, 4, 2, 1, 7>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
-  } else if (np == NP_F16) {   // forward only (no pmode / dgrad instantiations)
-    if (pmode >= 0) return;
+  } else if (np == NP_F16) {
     if (cout == 128)
       launch_x3<NP_F16, 8, 4, 2, 2, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 64)
@@ -1163,7 +1185,8 @@ extern "C" int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpa
                                                  ebsdvae_stream_t stream) {
   X3Cfg c;
   EV_REQUIRE(g && wpack && gin && B > 0, "conv3x3_dgrad_inbwd_split: null pointer or empty batch");
-  EV_REQUIRE(pieces != NP_F16, "conv3x3_dgrad_inbwd_split: fp16 pieces are forward-only");
+  EV_REQUIRE(pieces != NP_F16, "conv3x3_dgrad_inbwd_split: fp16 pieces need the gradient scale "
+             "(ebsdvae_conv3x3_dgrad_inbwd_f16)");
   EV_REQUIRE(pmode >= -1 && pmode <= P_UPSUM, "conv3x3_dgrad_inbwd_split: bad pmode %d", pmode);
   EV_REQUIRE(pmode != P_UPSUM || ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, pieces),
              "conv3x3_dgrad_inbwd_split: summed upsample adjoint unsupported for H=%d W=%d", H, W);
@@ -1179,4 +1202,30 @@ extern "C" int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpa
   dispatch_split(c, pieces, g, nullptr, ACT_RAW, wpack, nullptr, gin, nullptr, nullptr, B, H, W, cin,
                  cout, (hipStream_t)stream, pmode, f);
   return evh::check_launch("conv3x3_dgrad_inbwd_split");
+}
+
+extern "C" int ebsdvae_conv3x3_dgrad_inbwd_f16(const float* g, const float* gmax, int gm_tiles,
+                                               const void* wpack, float* gin, const float* y_prev,
+                                               const float* st_prev, int pmode, double* part, int B,
+                                               int H, int W, int cin, int cout,
+                                               ebsdvae_stream_t stream) {
+  X3Cfg c;
+  EV_REQUIRE(g && gmax && gm_tiles > 0 && wpack && gin && B > 0,
+             "conv3x3_dgrad_inbwd_f16: null pointer, empty batch or no gradient maxima");
+  EV_REQUIRE(pmode >= -1 && pmode <= P_UPSUM, "conv3x3_dgrad_inbwd_f16: bad pmode %d", pmode);
+  EV_REQUIRE(pmode != P_UPSUM || ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, NP_F16),
+             "conv3x3_dgrad_inbwd_f16: summed upsample adjoint unsupported for H=%d W=%d", H, W);
+  EV_REQUIRE(pmode < 0 || (y_prev && st_prev && part && (W & (W - 1)) == 0),
+             "conv3x3_dgrad_inbwd_f16: fused reduce needs y_prev, st_prev, part and W = 2^k");
+  EV_REQUIRE(plan_split(H, W, cin, cout, NP_F16, &c),
+             "conv3x3_dgrad_inbwd_f16: unsupported shape H=%d W=%d cin=%d cout=%d", H, W, cin, cout);
+  InBwdFuse f;
+  f.yprev = y_prev;
+  f.stprev = (const float2*)st_prev;
+  f.part = (double2*)part;
+  f.gmax = gmax;
+  f.gmT = gm_tiles;
+  dispatch_split(c, NP_F16, g, nullptr, ACT_RAW, wpack, nullptr, gin, nullptr, nullptr, B, H, W, cin,
+                 cout, (hipStream_t)stream, pmode, f);
+  return evh::check_launch("conv3x3_dgrad_inbwd_f16");
 }

@@ -104,8 +104,9 @@ template <bool APPLY>
 __global__ __launch_bounds__(256) void in_bwd_kernel(
     const float* __restrict__ gnext, int pmode, const float* __restrict__ y,
     const float2* __restrict__ st, const float2* __restrict__ bst, double2* __restrict__ part,
-    float* __restrict__ gy, int H, int W, int C, int T) {
+    float* __restrict__ gy, int H, int W, int C, int T, float* __restrict__ gmax) {
   __shared__ double red[2][4][256];
+  float amax = 0.f;   // APPLY: max |gy| of this thread (gmax: per-tile maxima for the f16 dgrad)
   const int tile = blockIdx.x, b = blockIdx.y;
   const int CG = C >> 2;
   const int tid = threadIdx.x;
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
             const float x = xh[k][ch];
             const float gx = (arg[ch] == k) ? gv[ch] * slope(x) : 0.f;
             o[ch] = rstd[ch] * (gx - m1[ch] - x * m2[ch]);
+            amax = fmaxf(amax, fabsf(o[ch]));
           }
           st4(gyb + poff[k], make_float4(o[0], o[1], o[2], o[3]));
         }
@@ -212,10 +214,19 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
           a2[ch] = fma((double)gx, (double)x, a2[ch]);
         } else {
           o[ch] = rstd[ch] * (gx - m1[ch] - x * m2[ch]);
+          amax = fmaxf(amax, fabsf(o[ch]));
         }
       }
       if (APPLY) st4(gyb + (size_t)p * C + c, make_float4(o[0], o[1], o[2], o[3]));
     }
+  }
+  if (APPLY && gmax) {   // block-uniform: one maximum per (image, tile)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+    __shared__ float wmax[4];
+    if ((tid & 63) == 0) wmax[tid >> 6] = amax;
+    __syncthreads();
+    if (tid == 0) gmax[(size_t)b * T + tile] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
   }
   if (!APPLY) {
 #pragma unroll
@@ -561,7 +572,7 @@ extern "C" int ebsdvae_in_bwd_reduce(const float* gnext, int pmode, const float*
   const int T = in_bwd_tiles_host(H, W);
   hipLaunchKernelGGL(in_bwd_kernel<false>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
                      pmode, y, (const float2*)stats, (const float2*)nullptr, (double2*)part,
-                     (float*)nullptr, H, W, C, T);
+                     (float*)nullptr, H, W, C, T, (float*)nullptr);
   return evh::check_launch("in_bwd_reduce");
 }
 
@@ -574,19 +585,36 @@ extern "C" int ebsdvae_in_bwd_finalize(const double* part, float* bstats, int B,
   return evh::check_launch("in_bwd_finalize");
 }
 
+// the apply pass keeps no per-tile partials: split the planes finer than the reduce so
+// small maps still put >= 2048 workgroups (8 per CU) in flight
+static int in_bwd_apply_tiles_host(int B, int H, int W) {
+  int T = in_bwd_tiles_host(H, W);
+  while (B * T < 2048 && H % (2 * T) == 0 && ((H / (2 * T)) & 1) == 0) T *= 2;
+  return T;
+}
+
+extern "C" int ebsdvae_in_bwd_apply_tiles(int B, int H, int W, int C) {
+  (void)C;
+  return in_bwd_apply_tiles_host(B, H, W);
+}
+
+extern "C" int ebsdvae_in_bwd_apply_max(const float* gnext, int pmode, const float* y,
+                                        const float* stats, const float* bstats, float* gy,
+                                        float* gmax, int B, int H, int W, int C,
+                                        ebsdvae_stream_t stream) {
+  EV_REQUIRE(gnext && y && stats && bstats && gy, "in_bwd_apply: null pointer");
+  EV_REQUIRE(pmode >= 0 && pmode <= 2 && C % 4 == 0 && (256 % (C / 4)) == 0, "in_bwd_apply: bad pmode/C");
+  const int T = in_bwd_apply_tiles_host(B, H, W);
+  hipLaunchKernelGGL(in_bwd_kernel<true>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
+                     pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy, H,
+                     W, C, T, gmax);
+  return evh::check_launch("in_bwd_apply");
+}
+
 extern "C" int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* y,
                                     const float* stats, const float* bstats, float* gy, int B,
                                     int H, int W, int C, ebsdvae_stream_t stream) {
-  EV_REQUIRE(gnext && y && stats && bstats && gy, "in_bwd_apply: null pointer");
-  EV_REQUIRE(pmode >= 0 && pmode <= 2 && C % 4 == 0 && (256 % (C / 4)) == 0, "in_bwd_apply: bad pmode/C");
-  // the apply pass keeps no per-tile partials: split the planes finer than the reduce so
-  // small maps still put >= 2048 workgroups (8 per CU) in flight
-  int T = in_bwd_tiles_host(H, W);
-  while (B * T < 2048 && H % (2 * T) == 0 && ((H / (2 * T)) & 1) == 0) T *= 2;
-  hipLaunchKernelGGL(in_bwd_kernel<true>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
-                     pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy, H,
-                     W, C, T);
-  return evh::check_launch("in_bwd_apply");
+  return ebsdvae_in_bwd_apply_max(gnext, pmode, y, stats, bstats, gy, nullptr, B, H, W, C, stream);
 }
 
 // ------------------------------------------------------------------ network-end fusions (ABI)

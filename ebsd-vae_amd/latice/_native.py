@@ -38,6 +38,7 @@ SIGNATURES = {
     "ebsdvae_conv3x3_split_pool_ok": [I, I, I, I, I],
     "ebsdvae_conv3x3_fwd_split_pooled": [P, P, I, P, P, P, P, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_dgrad_inbwd_split": [P, P, P, P, P, I, P, I, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_dgrad_inbwd_f16": [P, P, I, P, P, P, P, I, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_fwd": [P, P, I, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],
     "ebsdvae_conv3x3_wgrad_slices": [I, I, I, I, I],
@@ -54,6 +55,8 @@ SIGNATURES = {
     "ebsdvae_in_bwd_reduce": [P, I, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_finalize": [P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_apply": [P, I, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_apply_tiles": [I, I, I, I],
+    "ebsdvae_in_bwd_apply_max": [P, I, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_upsample2_bwd": [P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_final_reduce": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_final_apply": [P, P, P, P, P, P, I, I, I, I, P],
@@ -84,7 +87,7 @@ _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": 
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
            "ebsdvae_wgrad_reduce_batch_work", "ebsdvae_cosine_topk_work",
-           "ebsdvae_in_bwd_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
+           "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
            "ebsdvae_conv3x3_split_pool_ok",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices"}

@@ -180,9 +180,10 @@ def _empty(*shape, like):
 #   "fp32"   v_mfma_f32_32x32x2_f32 (exact fp32 products);
 #   "bf16x6" 3-piece split-bf16 MFMA, 6 products per fp32 product (~2^-25, fp32 grade);
 #   "bf16x3" 2-piece split-bf16 MFMA, 3 products (~2^-16.5 per product);
-#   "f16x3"  forward convs on 2-piece split-fp16 MFMA (x0 = f16(x), x1 = f16(x - x0); weights
-#            packed x256), 3 products (~2^-22.5 per product); input / weight gradients on
-#            bf16x6 (gradients span magnitudes below fp16's range).
+#   "f16x3"  forward and input-gradient convs on 2-piece split-fp16 MFMA (x0 = f16(x),
+#            x1 = f16(x - x0); weights packed x256; the gradient operand of each image scaled
+#            by a power of two from the max |gy| the InstanceNorm-backward apply emits),
+#            3 products (~2^-22.5 per product); weight gradients on bf16x6.
 # Split modes cover every conv layer the split kernel supports (Cout in {32,64,128},
 # H*W >= 256, plus the 8x8 maps for bf16x6); the others stay fp32.
 PIECES_F16 = 16   # EBSDVAE_PIECES_F16 (include/ebsdvae.h)
@@ -225,14 +226,15 @@ def _supported(H: int, cin: int, cout: int, np_: int) -> bool:
     return _SPLIT_CACHE[key]
 
 
-def split_pieces(H: int, cin: int, cout: int, dgrad: bool = False) -> int:
+def split_pieces(H: int, cin: int, cout: int, dgrad: bool = False, scaled: bool = False) -> int:
     """Piece format of a conv with input channels cin -> cout at HxH: bf16 pieces per operand
-    (2 or 3), PIECES_F16, or 0 = fp32.  dgrad: the input-gradient pack (never fp16)."""
+    (2 or 3), PIECES_F16, or 0 = fp32.  dgrad: the input-gradient pack, fp16 only when its
+    gradient operand comes with per-tile maxima (scaled: in_backward(..., gmax=True))."""
     np_ = _PIECES[_PRECISION]
     if np_ == 0:
         return 0
     f16 = _FWD_PIECES.get(_PRECISION)
-    if f16 and not dgrad and _supported(H, cin, cout, f16):
+    if f16 and (not dgrad or scaled) and _supported(H, cin, cout, f16):
         return f16
     return np_ if _supported(H, cin, cout, np_) else 0
 
@@ -273,24 +275,25 @@ class PackSet:
         descs = {}
         for i, L in enumerate(plan.enc):
             self._add(L, params[L.name + ".weight"], dgrad=i > 0, descs=descs)
-        for L in plan.dec:
-            self._add(L, params[L.name + ".weight"], dgrad=True, descs=descs)
+        for L in plan.dec:   # the last block's gy comes from in_backward_final (no maxima)
+            self._add(L, params[L.name + ".weight"], dgrad=True, descs=descs,
+                      scaled=L is not plan.dec[-1])
         self.batches = []
         for np_, lst in sorted(descs.items()):
             if len(lst) > N.MAX_PACK:
                 raise RuntimeError(f"PackSet: {len(lst)} packs > {N.MAX_PACK}")
             self.batches.append((np_, (N.PackDesc * len(lst))(*lst), len(lst)))
 
-    def _one(self, L, w, dgrad, descs):
+    def _one(self, L, w, dgrad, descs, scaled=True):
         ci_, co_ = (L.cout, L.cin) if dgrad else (L.cin, L.cout)
-        np_ = split_pieces(L.H, ci_, co_, dgrad)
+        np_ = split_pieces(L.H, ci_, co_, dgrad, scaled)
         t = _empty(_pack_numel(L, np_, dgrad), like=w)
         descs.setdefault(np_, []).append(N.PackDesc(N.ptr(w), N.ptr(t), L.cin, L.cout, L.kind, int(dgrad)))
         return PackedW(t, np_)
 
-    def _add(self, L, w, dgrad, descs):
+    def _add(self, L, w, dgrad, descs, scaled=True):
         pf = self._one(L, w, False, descs)
-        pd = self._one(L, w, True, descs) if dgrad else None
+        pd = self._one(L, w, True, descs, scaled) if dgrad else None
         self.packs[L.name] = (pf, pd)
 
     def refresh(self):
@@ -369,8 +372,16 @@ def in_backward(gnext, pmode, y, st, part=None):
     bst = _empty(B, C, 2, like=y)
     N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, T, H * W, s)
     gy = torch.empty_like(y)
-    N.call("ebsdvae_in_bwd_apply", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
-           N.ptr(gy), B, H, W, C, s)
+    if _FWD_PIECES.get(_PRECISION):
+        # per-tile max |gy|: the scale of the split-fp16 input-gradient conv that consumes gy
+        Tg = N.call("ebsdvae_in_bwd_apply_tiles", B, H, W, C)
+        gmax = _empty(B, Tg, like=y)
+        N.call("ebsdvae_in_bwd_apply_max", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
+               N.ptr(gy), N.ptr(gmax), B, H, W, C, s)
+        gy.ev_gmax = gmax
+    else:
+        N.call("ebsdvae_in_bwd_apply", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
+               N.ptr(gy), B, H, W, C, s)
     return gy
 
 
@@ -502,6 +513,25 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
         gin = _empty(B, H, W, layer.cin, like=gy)
     tag = f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}"
     flops = conv_flops(B, H, W, layer.cin, layer.cout)
+    if wd.pieces == PIECES_F16:
+        gmax = getattr(gy, "ev_gmax", None)
+        if gmax is None:
+            raise RuntimeError("conv_dgrad: split-fp16 input gradient needs gy's per-tile maxima "
+                               "(in_backward under f16x3)")
+        part = None
+        if prev is None:
+            yp = sp = pptr = None
+            pmode = -1
+        else:
+            y_prev, st_prev, pmode = prev
+            T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, W, layer.cin)
+            part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
+            yp, sp, pptr = N.ptr(y_prev), N.ptr(st_prev), part.data_ptr()
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_f16", N.ptr(gy),
+                N.ptr(gmax), gmax.shape[1], N.ptr(wd.t), N.ptr(gin), yp, sp, pmode, pptr, B, H, W,
+                layer.cout, layer.cin, N.stream(), tag=tag + ("" if prev is None else " +inbwd"),
+                pieces=wd.pieces)
+        return gin if prev is None else (gin, part)
     if prev is None:
         if wd.pieces:
             _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_split", N.ptr(gy),

@@ -142,6 +142,16 @@ int ebsdvae_conv3x3_dgrad_inbwd_split(const float* g, const void* wpack, float* 
                                       const float* y_prev, const float* st_prev, int pmode,
                                       double* part, int B, int H, int W, int cin, int cout,
                                       int pieces, ebsdvae_stream_t stream);
+/* Input gradient on split-fp16 pieces (pieces = EBSDVAE_PIECES_F16, wpack from
+ * ebsdvae_pack_conv_weights_split with for_dgrad = 1): as ebsdvae_conv3x3_dgrad_inbwd_split,
+ * but g is scaled per image by 2^k (k such that max|g[b]| * 2^k lies in [2^11, 2^12)) before
+ * the fp16 split and unscaled in the epilogue, so gradients of any magnitude keep fp16's 22
+ * significand bits.  gmax: (B, gm_tiles) per-tile maxima of |g| from
+ * ebsdvae_in_bwd_apply_max (gm_tiles = ebsdvae_in_bwd_apply_tiles). */
+int ebsdvae_conv3x3_dgrad_inbwd_f16(const float* g, const float* gmax, int gm_tiles,
+                                    const void* wpack, float* gin, const float* y_prev,
+                                    const float* st_prev, int pmode, double* part, int B, int H,
+                                    int W, int cin, int cout, ebsdvae_stream_t stream);
 
 /* ---- weight gradients (deterministic two-level reduction) -----------------------------
  * Partial dW[co][ci][tap] and db[co] over pixel slices; then ebsdvae_wgrad_reduce sums
@@ -205,6 +215,12 @@ int ebsdvae_in_bwd_finalize(const double* part, float* bstats, int B, int C, int
 int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* y, const float* stats,
                          const float* bstats, float* gy, int B, int H, int W, int C,
                          ebsdvae_stream_t stream);
+/* As ebsdvae_in_bwd_apply, and also writes gmax[b * T + t] = max |gy| over tile t of image b
+ * (T = ebsdvae_in_bwd_apply_tiles(B, H, W, C) row bands per image; gmax may be NULL). */
+int ebsdvae_in_bwd_apply_tiles(int B, int H, int W, int C);
+int ebsdvae_in_bwd_apply_max(const float* gnext, int pmode, const float* y, const float* stats,
+                             const float* bstats, float* gy, float* gmax, int B, int H, int W,
+                             int C, ebsdvae_stream_t stream);
 /* Network-end fusions (C == 32; slices = B * ebsdvae_in_bwd_tiles(H,W,C) partials for
  * ebsdvae_wgrad_reduce):
  *  final_*: the block feeding the last conv (latice/model.py:147-148).  Its output gradient

@@ -531,6 +531,61 @@ def test_dgrad_fused_split_bf16(cuda, cin, cout, H, pmode, prec):
     assert O.rel_err(host(g_prev), ref) < 2e-4
 
 
+def _pack_f16_dgrad(w_d, layer):
+    import ctypes
+    numel = N.call("ebsdvae_pack_split_bytes", layer.cout, layer.cin, E.PIECES_F16) // 4
+    out = torch.empty(numel, dtype=torch.float32, device=w_d.device)
+    d = (N.PackDesc * 1)(N.PackDesc(N.ptr(w_d), N.ptr(out), layer.cin, layer.cout, layer.kind, 1))
+    N.call("ebsdvae_pack_conv_weights_split", ctypes.addressof(d), 1, E.PIECES_F16, N.stream())
+    return E.PackedW(out, E.PIECES_F16)
+
+
+@pytest.mark.parametrize("gscale", [1.0, 1e-7])
+@pytest.mark.parametrize("cin,cout,H,pmode", [c for c in FUSED_CASES if c[2] >= 16])
+def test_dgrad_fused_split_f16(cuda, cin, cout, H, pmode, gscale):
+    """Split-fp16 input gradient (f16x3) == float64 oracle at 2e-5, with the gradient operand
+    scaled per image from its maximum: images 1e3 apart in magnitude, and tiny gradients
+    (1e-7: far below fp16's normal range unscaled).  Also pins the per-tile maxima that the
+    InstanceNorm-backward apply emits (ebsdvae_in_bwd_apply_max)."""
+    if not N.call("ebsdvae_conv3x3_split_supported", H, H, cout, cin, E.PIECES_F16):
+        pytest.skip("shape not covered by the split kernel")
+    rng = np.random.default_rng(43 + cin + cout + H + pmode)
+    B = 2
+    Hy = {E.P_ID: H, E.P_POOL: 2 * H, E.P_UP: H // 2}[pmode]
+    y = rng.standard_normal((B, Hy, Hy, cin)) * 2 + 0.5
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    gy = rng.standard_normal((B, H, H, cout)) * gscale
+    gy[1] *= 1e3
+    wsrc = rng.standard_normal((cout, cin, 3, 3)) * 0.1
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, E.ACT_RAW, 0)
+    with E.precision("f16x3"):
+        y_d, st_d, w_d = dev(y), dev(st), dev(wsrc)
+        wd = _pack_f16_dgrad(w_d, layer)
+        g_d = dev(gy)
+        g_d.ev_gmax = dev(np.abs(gy).reshape(B, -1).max(1, keepdims=True))
+        gin, part = E.conv_dgrad(g_d, layer, w_d, prev=(y_d, st_d, pmode), wd=wd)
+        g_prev = E.in_backward(gin, pmode, y_d, st_d, part=part)
+        gin2 = E.conv_dgrad(g_d, layer, w_d, wd=wd)
+        gmax = host(g_prev.ev_gmax)
+    gn = O.conv3x3_dgrad(gy, wsrc)
+    for b in range(B):   # per image: the two differ by 1e3 in magnitude
+        assert O.rel_err(host(gin)[b], gn[b]) < SPLIT_TOL["f16x3"], b
+        assert O.rel_err(host(gin2)[b], gn[b]) < SPLIT_TOL["f16x3"], b
+    a = O.lrelu(xh)
+    if pmode == E.P_POOL:
+        _, arg = O.maxpool2(a)
+        ga = O.maxpool2_bwd(gn, arg)
+    elif pmode == E.P_UP:
+        ga = O.upsample2_bwd(gn)
+    else:
+        ga = gn
+    ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
+    for b in range(B):
+        assert O.rel_err(host(g_prev)[b], ref[b]) < 2e-4, b
+    assert np.array_equal(gmax.max(1), np.abs(host(g_prev)).reshape(B, -1).max(1))
+
+
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
 @pytest.mark.parametrize("cin,cout,H,mode,kind", [c for c in WG_CASES if c[0] >= 32 and c[1] >= 32])
 def test_conv_wgrad_split_bf16(cuda, cin, cout, H, mode, kind, prec):
