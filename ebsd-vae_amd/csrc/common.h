@@ -107,6 +107,33 @@ EV_DEVINL float wave_sum(float v) {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// ---- split-fp16 piece format ("f16x3", include/ebsdvae.h EBSDVAE_PIECES_F16): two fp16
+// pieces x0 = f16(x), x1 = f16(x - x0) per operand, products a0b0 + a0b1 + a1b0 on the fp16
+// MFMA.  Weights are packed as w * kF16WScale; gradient operands are scaled by a power of
+// two from their maximum (f16_shift) so that both sit inside fp16's range.
+constexpr int NP_F16 = 16;   // == EBSDVAE_PIECES_F16
+constexpr float kF16WScale = 256.f;
+constexpr int npc(int np) { return np == NP_F16 ? 2 : np; }   // pieces per operand
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// k such that m * 2^k lies in [2^11, 2^12) (0 for a zero / non-finite maximum)
+EV_DEVINL int f16_shift_of(float m) {
+  if (!(m > 0.f) || !(m <= 3.4e38f)) return 0;
+  int e;
+  (void)frexpf(m, &e);   // m = f * 2^e, f in [0.5, 1)
+  return min(max(12 - e, -100), 100);
+}
+// the shift of images [b0, b1] from per-tile maxima gmax (B, gmT) (0 without them)
+EV_DEVINL int f16_gshift(const float* __restrict__ gmax, int gmT, int b0, int b1) {
+  if (!gmax) return 0;
+  float m = 0.f;
+  for (size_t i = (size_t)b0 * gmT; i < (size_t)(b1 + 1) * gmT; ++i) m = fmaxf(m, gmax[i]);
+  return f16_shift_of(m);
+}
+EV_DEVINL int f16_gshift(const float* __restrict__ gmax, int gmT, int b) {
+  return f16_gshift(gmax, gmT, b, b);
+}
+
 }  // namespace ev
 
 // ---------------------------------------------------------------- host-side error plumbing

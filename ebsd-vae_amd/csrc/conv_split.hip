@@ -28,6 +28,8 @@
 
 namespace ev {
 
+static_assert(NP_F16 == EBSDVAE_PIECES_F16, "piece-format id");
+
 #ifdef EV_PIPE_TRACE   // diagnostic build only: per-wave cycle split of conv3x3_pipe_kernel
 __device__ unsigned long long ev_pipe_trace[4096 * 8 * 6];
 #define EV_T(x) unsigned long long x = __builtin_amdgcn_s_memtime()
@@ -68,9 +70,6 @@ EV_DEVINL void split_bf16(float x, __bf16 (&p)[NP]) {
 // |w| < 255 stays finite) and the epilogue multiplies the accumulators by the exact inverse.
 // The forward operands are normalised activations (IN + LeakyReLU, |x| <= sqrt(H*W)), which
 // fp16 holds; gradients span far smaller magnitudes, so dgrad / wgrad stay on bf16x6.
-constexpr int NP_F16 = EBSDVAE_PIECES_F16;
-constexpr float kF16WScale = 256.f;
-constexpr int npc(int np) { return np == NP_F16 ? 2 : np; }   // pieces per operand
 
 template <int NP>
 EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
@@ -91,20 +90,6 @@ EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
   }
 }
 
-// NP_F16 input gradient: the gradient operand of image b is scaled by 2^k, k such that
-// max|g[b]| * 2^k lies in [2^11, 2^12), from the per-tile maxima (B, gmT) that the
-// InstanceNorm-backward apply wrote (0 without them, or for a zero / non-finite maximum)
-EV_DEVINL int f16_gshift(const float* __restrict__ gmax, int gmT, int b) {
-  if (!gmax) return 0;
-  float m = 0.f;
-  for (int t = 0; t < gmT; ++t) m = fmaxf(m, gmax[(size_t)b * gmT + t]);
-  if (!(m > 0.f) || !(m <= 3.4e38f)) return 0;
-  int e;
-  (void)frexpf(m, &e);   // m = f * 2^e, f in [0.5, 1)
-  return min(max(12 - e, -100), 100);
-}
-
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 // one 32x32x16 product of two piece fragments (bf16, or fp16 bits for NP_F16)
 template <int NP>
 EV_DEVINL f32x16 mfma_piece(bf16x8 a, bf16x8 b, f32x16 c) {

@@ -354,19 +354,36 @@ template <int NP>
 EV_DEVINL void store_pieces(char* base, size_t piece_stride, float4 v) {
   const float e[4] = {v.x, v.y, v.z, v.w};
   typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
-  bf4 pc[NP];
+  constexpr int NPC = npc(NP);
+  bf4 pc[NPC];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    float r = e[c];
+    if constexpr (NP == NP_F16) {   // fp16 bit patterns in the 16-bit piece slots
+      const _Float16 h0 = (_Float16)e[c];
+      const _Float16 h1 = (_Float16)(e[c] - (float)h0);
+      pc[0][c] = __builtin_bit_cast(__bf16, h0);
+      pc[1][c] = __builtin_bit_cast(__bf16, h1);
+    } else {
+      float r = e[c];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const __bf16 h = (__bf16)r;
-      pc[i][c] = h;
-      r -= (float)h;
+      for (int i = 0; i < NP; ++i) {
+        const __bf16 h = (__bf16)r;
+        pc[i][c] = h;
+        r -= (float)h;
+      }
     }
   }
 #pragma unroll
-  for (int i = 0; i < NP; ++i) *reinterpret_cast<bf4*>(base + i * piece_stride) = pc[i];
+  for (int i = 0; i < NPC; ++i) *reinterpret_cast<bf4*>(base + i * piece_stride) = pc[i];
+}
+
+template <int NP>
+EV_DEVINL f32x4 mfma16_piece(bf16x8w a, bf16x8w b, f32x4 c) {
+  if constexpr (NP == NP_F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 constexpr int WGS_ASB = 96;   // activation image row stride (32 ch x 2 B + 32 B)
@@ -375,8 +392,10 @@ template <int NP, int NWCO, int KSPLIT, int MODE, int TW, int PT>
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats,
     const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
-    int H, int W, int Cin, int Cout, WgGeom g) {
+    int H, int W, int Cin, int Cout, WgGeom g, const float* __restrict__ gmax, int gmT) {
   using T = WgTileP<TW, PT>;
+  constexpr int NPC = npc(NP);
+  constexpr bool F16 = NP == NP_F16;
   constexpr int CO_T = NWCO * 32;
   constexpr int GSB = CO_T * 2 + 32;      // gy image row stride (bytes)
   constexpr int QG = CO_T / 4;
@@ -392,7 +411,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
   static_assert(MODE != ACT_NORM_POOL, "pool-fed layers use the materialised activation");
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   char* gimg = wsm;                         // [NP][PT][GSB]
-  char* aimg = wsm + NP * GY_PIECE;         // [NP][HALO][96]
+  char* aimg = wsm + NPC * GY_PIECE;        // [NP][HALO][96]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
   const int slice = blockIdx.x, co0 = blockIdx.y * CO_T, ci0 = blockIdx.z * 32;
@@ -411,6 +430,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
   const int per_img = g.ntx * g.nty;
   const int t_beg = slice * g.tps;
   const int t_end = min(t_beg + g.tps, g.tiles);
+  // F16: the slice's gy is scaled by 2^k from the maximum over the images it covers
+  // (a common scale: the accumulators sum over all of them), undone at the partial store
+  int gshift = 0;
+  if constexpr (F16) {
+    static_assert(T::NI == 1, "one image per tile");
+    if (t_beg < t_end) gshift = f16_gshift(gmax, gmT, t_beg / per_img, (t_end - 1) / per_img);
+  }
+  const float gsc = ldexpf(1.f, gshift);
   float4 rg[KG], rh[KH];
   float2 st[T::NI][4];
   int cb0 = 0, cy0 = 0, cx0 = 0;
@@ -466,6 +493,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
       float4 v = rg[k];
       if (T::NI > 1 && cb0 + px / T::IPX >= B) v = make_float4(0.f, 0.f, 0.f, 0.f);
       tb.x += v.x; tb.y += v.y; tb.z += v.z; tb.w += v.w;
+      if constexpr (F16) v = make_float4(v.x * gsc, v.y * gsc, v.z * gsc, v.w * gsc);
       store_pieces<NP>(gimg + px * GSB + qg * 8, GY_PIECE, v);
     }
     bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
@@ -508,9 +536,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
 #pragma unroll
     for (int s = wk; s < KSTEPS; s += KSPLIT) {
       const int px0 = 32 * s + 4 * gq + q, px1 = px0 + 16;   // rows of read 0 / read 1
-      bf16x8w a[NP][2];
+      bf16x8w a[NPC][2];
 #pragma unroll
-      for (int i = 0; i < NP; ++i)
+      for (int i = 0; i < NPC; ++i)
 #pragma unroll
         for (int f = 0; f < 2; ++f)
           a[i][f] = tr_frag(gimg + i * GY_PIECE + px0 * GSB + acol + f * 32,
@@ -525,29 +553,29 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int toff = (tap / 3) * T::WP + tap % 3;
-        bf16x8w b[NP];
+        bf16x8w b[NPC];
 #pragma unroll
-        for (int i = 0; i < NP; ++i)
+        for (int i = 0; i < NPC; ++i)
           b[i] = tr_frag(aimg + i * ACT_PIECE + (hp0 + toff) * WGS_ASB + bcol,
                          aimg + i * ACT_PIECE + (hp1 + toff) * WGS_ASB + bcol);
 #ifdef EV_WG_NOMFMA   // timing experiment only (wrong results)
 #pragma unroll
         for (int f = 0; f < 2; ++f)
 #pragma unroll
-          for (int i = 0; i < NP; ++i) acc[f][tap][i & 3] += (float)a[i][f][0] * (float)b[i][1];
+          for (int i = 0; i < NPC; ++i) acc[f][tap][i & 3] += (float)a[i][f][0] * (float)b[i][1];
         if (false)
 #endif
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           f32x4 c = acc[f][tap];
-          if (NP == 3) {
+          if constexpr (NP == 3) {
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][f], b[1], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[NP - 1][f], b[0], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][f], b[NP - 1], c, 0, 0, 0);
           }
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][f], b[0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][f], b[1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][f], b[0], c, 0, 0, 0);
+          c = mfma16_piece<NP>(a[1][f], b[0], c);
+          c = mfma16_piece<NP>(a[0][f], b[1], c);
+          c = mfma16_piece<NP>(a[0][f], b[0], c);
           acc[f][tap] = c;
         }
       }
@@ -586,7 +614,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + wco * 32 + f * 16 + (lane >> 4) * 4 + r;
-          wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] = acc[f][tap][r];
+          wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] =
+              F16 ? acc[f][tap][r] * (1.f / gsc) : acc[f][tap][r];
         }
   }
   if (do_bias) {
@@ -894,10 +923,10 @@ static void launch_wg(dim3 grid, size_t lds, hipStream_t s, const float* src, co
 template <int NP, int NWCO, int KSPLIT, int MODE, int TW, int PT>
 static void launch_wgs_tw(dim3 grid, hipStream_t s, const float* src, const float* st,
                           const float* gy, float* wpart, float* bpart, int B, int H, int W, int cin,
-                          int cout, const WgGeom& g) {
+                          int cout, const WgGeom& g, const float* gmax, int gmT) {
   using T = WgTileP<TW, PT>;
   constexpr int CO_T = NWCO * 32;
-  const size_t lds_img = (size_t)NP * ((size_t)PT * (CO_T * 2 + 32) + (size_t)T::HALO * WGS_ASB);
+  const size_t lds_img = (size_t)npc(NP) * ((size_t)PT * (CO_T * 2 + 32) + (size_t)T::HALO * WGS_ASB);
   const size_t lds_fold = KSPLIT == 2 ? (size_t)2 * 72 * 64 * 4 : 0;
   const size_t lds_bias = 256 * 4 * 8;
   size_t lds = lds_img;
@@ -910,39 +939,39 @@ static void launch_wgs_tw(dim3 grid, hipStream_t s, const float* src, const floa
     once = true;
   }
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, (const float2*)st, gy, wpart, bpart, B, H, W,
-                     cin, cout, g);
+                     cin, cout, g, gmax, gmT);
 }
 
 template <int NP, int NWCO, int KSPLIT, int MODE>
 static void launch_wgs(dim3 grid, hipStream_t s, const float* src, const float* st, const float* gy,
                        float* wpart, float* bpart, int B, int H, int W, int cin, int cout,
-                       const WgGeom& g) {
+                       const WgGeom& g, const float* gmax, int gmT) {
   constexpr int PT = 64;
   if (g.TW == 32)
-    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 32, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 32, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT);
   else if (g.TW == 16)
-    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 16, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 16, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT);
   else if constexpr (NWCO == 1)
-    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 8, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g);
+    launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 8, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT);
 }
 
 template <int NP>
 static void dispatch_wgs(int mode, bool narrow, dim3 grid, hipStream_t s, const float* src,
                          const float* st, const float* gy, float* wpart, float* bpart, int B, int H,
-                         int W, int cin, int cout, const WgGeom& g) {
+                         int W, int cin, int cout, const WgGeom& g, const float* gmax, int gmT) {
   if (narrow) {
     switch (mode) {
-      case ACT_RAW: launch_wgs<NP, 1, 2, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
-      case ACT_NORM: launch_wgs<NP, 1, 2, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
-      case ACT_UP: launch_wgs<NP, 1, 2, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
-      default: launch_wgs<NP, 1, 2, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_RAW: launch_wgs<NP, 1, 2, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_NORM: launch_wgs<NP, 1, 2, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_UP: launch_wgs<NP, 1, 2, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      default: launch_wgs<NP, 1, 2, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
     }
   } else {
     switch (mode) {
-      case ACT_RAW: launch_wgs<NP, 2, 1, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
-      case ACT_NORM: launch_wgs<NP, 2, 1, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
-      case ACT_UP: launch_wgs<NP, 2, 1, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
-      default: launch_wgs<NP, 2, 1, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g); break;
+      case ACT_RAW: launch_wgs<NP, 2, 1, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_NORM: launch_wgs<NP, 2, 1, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_UP: launch_wgs<NP, 2, 1, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      default: launch_wgs<NP, 2, 1, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
     }
   }
 }
@@ -961,7 +990,7 @@ using namespace ev;
 
 extern "C" int ebsdvae_conv3x3_wgrad_split_slices(int B, int H, int W, int cin, int cout, int pieces) {
   WgGeom g;
-  if (pieces != 2 && pieces != 3) return -1;
+  if (pieces != 2 && pieces != 3 && pieces != NP_F16) return -1;
   if (cin % 32 || !(cout == 32 || cout % 64 == 0)) return -1;
   const int pt = 64;
   if (!wg_geom(B, H, W, cin, cout, &g, pt) || !wgs_geom_ok(g, pt)) return -1;
@@ -989,10 +1018,35 @@ extern "C" int ebsdvae_conv3x3_wgrad_split(const float* src, const float* src_st
   const bool narrow = cout == 32 || g.TW == 8 || (pieces == 3 && g.TW == 16);
   const dim3 grid(g.slices, narrow ? cout / 32 : cout / 64, cin / 32);
   if (pieces == 3)
-    dispatch_wgs<3>(src_mode, narrow, grid, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g);
+    dispatch_wgs<3>(src_mode, narrow, grid, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g,
+                    nullptr, 0);
   else
-    dispatch_wgs<2>(src_mode, narrow, grid, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g);
+    dispatch_wgs<2>(src_mode, narrow, grid, s, src, src_stats, gy, wpart, bpart, B, H, W, cin, cout, g,
+                    nullptr, 0);
   return evh::check_launch("wgrad_split");
+}
+
+extern "C" int ebsdvae_conv3x3_wgrad_f16(const float* src, const float* src_stats, int src_mode,
+                                         const float* gy, const float* gmax, int gm_tiles,
+                                         float* wpart, float* bpart, int B, int H, int W, int cin,
+                                         int cout, ebsdvae_stream_t stream) {
+  WgGeom g;
+  EV_REQUIRE(src && gy && gmax && gm_tiles > 0 && wpart && bpart && B > 0,
+             "conv3x3_wgrad_f16: null pointer or no gradient maxima");
+  EV_REQUIRE(src_mode >= 0 && src_mode <= 4 && src_mode != ACT_NORM_POOL,
+             "conv3x3_wgrad_f16: bad src_mode %d (pool-fed layers pass the pooled activation RAW)",
+             src_mode);
+  EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats, "conv3x3_wgrad_f16: NORM needs stats");
+  EV_REQUIRE(cin % 32 == 0 && (cout == 32 || cout % 64 == 0), "conv3x3_wgrad_f16: cin=%d cout=%d unsupported",
+             cin, cout);
+  const int pt = 64;
+  EV_REQUIRE(wg_geom(B, H, W, cin, cout, &g, pt) && wgs_geom_ok(g, pt),
+             "conv3x3_wgrad_f16: unsupported shape H=%d W=%d", H, W);
+  const bool narrow = cout == 32 || g.TW == 8;   // the 2-piece VGPR budget (as pieces = 2)
+  const dim3 grid(g.slices, narrow ? cout / 32 : cout / 64, cin / 32);
+  dispatch_wgs<NP_F16>(src_mode, narrow, grid, (hipStream_t)stream, src, src_stats, gy, wpart, bpart,
+                       B, H, W, cin, cout, g, gmax, gm_tiles);
+  return evh::check_launch("wgrad_f16");
 }
 
 extern "C" int ebsdvae_conv3x3_wgrad_slices(int B, int H, int W, int cin, int cout) {

@@ -45,6 +45,7 @@ SIGNATURES = {
     "ebsdvae_conv3x3_wgrad": [P, P, I, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_wgrad_split_slices": [I, I, I, I, I, I],
     "ebsdvae_conv3x3_wgrad_split": [P, P, I, P, P, P, I, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_wgrad_f16": [P, P, I, P, P, I, P, P, I, I, I, I, I, P],
     "ebsdvae_wgrad_reduce_work": [I, I, I],
     "ebsdvae_wgrad_reduce": [P, P, I, P, P, I, I, I, P, P],
     "ebsdvae_wgrad_reduce_batch_work": [P, I],

@@ -470,8 +470,26 @@ def in_backward_first(gnext, y, st, x, dw0, db0, part=None):
     _reduce_slices(wpart, bpart, S_, 1, C, KIND_CONV, dw0, db0)
 
 
-def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db):
+def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized=None):
+    """normalized: src is a normalised activation (default: the NORM modes); the split-fp16
+    weight gradient (f16x3, gy with per-tile maxima) scales only gy, so it needs one."""
     B, H, W, _ = gy.shape if gy.dim() == 4 else (*gy.shape, 1)
+    if normalized is None:
+        normalized = src_mode in (ACT_NORM, ACT_NORM_UP)
+    gmax = getattr(gy, "ev_gmax", None)
+    if (gmax is not None and normalized and _FWD_PIECES.get(_PRECISION)
+            and os.environ.get("EBSDVAE_WGRAD_F16", "1") != "0"):
+        S_ = N.call("ebsdvae_conv3x3_wgrad_split_slices", B, H, W, cin, cout, PIECES_F16)
+        if S_ > 0:
+            wpart = _empty(S_, 9, cout, cin, like=gy)
+            bpart = _empty(S_, cout, like=gy)
+            _launch("conv3x3_wgrad", conv_flops(B, H, W, cin, cout), N.call,
+                    "ebsdvae_conv3x3_wgrad_f16", N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(gy),
+                    N.ptr(gmax), gmax.shape[1], N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout,
+                    N.stream(), tag=f"wgrad {cin:3d}->{cout:3d} @{H:3d} m{src_mode} f16",
+                    pieces=PIECES_F16)
+            _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
+            return
     np_ = _PIECES[_PRECISION]
     S_ = N.call("ebsdvae_conv3x3_wgrad_split_slices", B, H, W, cin, cout, np_) if np_ else -1
     if S_ <= 0:
@@ -644,7 +662,8 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
         wn, bn = L.name + ".weight", L.name + ".bias"
         dw = _grad_buf(grads, wn, params[wn])
         db = _grad_buf(grads, bn, params[bn])
-        conv_wgrad(src, sst, mode, gy, L.cin, L.cout, L.kind, dw, db)
+        # every source but the raw input image is a normalised activation (.act_in included)
+        conv_wgrad(src, sst, mode, gy, L.cin, L.cout, L.kind, dw, db, normalized=i > 0)
         out[wn], out[bn] = dw, db
         if i > 0:
             P = plan.enc[i - 1]

@@ -172,6 +172,16 @@ int ebsdvae_conv3x3_wgrad_split_slices(int B, int H, int W, int cin, int cout, i
 int ebsdvae_conv3x3_wgrad_split(const float* src, const float* src_stats, int src_mode,
                                 const float* gy, float* wpart, float* bpart, int B, int H, int W,
                                 int cin, int cout, int pieces, ebsdvae_stream_t stream);
+/* Split-fp16 weight gradient (f16x3): as ebsdvae_conv3x3_wgrad_split with two fp16 pieces per
+ * operand on v_mfma_f32_16x16x32_f16.  gy of each slice is scaled by 2^k (k from the maximum
+ * of gmax over the images the slice covers, as ebsdvae_conv3x3_dgrad_inbwd_f16) and the
+ * partials are unscaled; the bias partials sum the unscaled gy.  The activation operand is
+ * not scaled, so src must be a normalised activation (NORM modes, or a materialised pooled
+ * activation passed RAW).  Slices: ebsdvae_conv3x3_wgrad_split_slices(..., EBSDVAE_PIECES_F16). */
+int ebsdvae_conv3x3_wgrad_f16(const float* src, const float* src_stats, int src_mode,
+                              const float* gy, const float* gmax, int gm_tiles, float* wpart,
+                              float* bpart, int B, int H, int W, int cin, int cout,
+                              ebsdvae_stream_t stream);
 int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
                          float* db, int cin, int cout, int kind, void* work,
                          ebsdvae_stream_t stream);
