@@ -154,7 +154,24 @@ def mfma_peak(pieces: int) -> float:
     return FP32_MFMA_TFLOPS if not pieces else BF16_MFMA_TFLOPS / {2: 3, 3: 6, PIECES_F16: 3}[pieces]
 
 
+_LAUNCHES = None
+
+
+@contextlib.contextmanager
+def record_launches():
+    """Test hook: the C-ABI entry points of the conv launches issued inside the block."""
+    global _LAUNCHES
+    outer, lst = _LAUNCHES, []
+    _LAUNCHES = lst
+    try:
+        yield lst
+    finally:
+        _LAUNCHES = outer
+
+
 def _launch(family, flops, fn, *args, tag=None, pieces=0):
+    if _LAUNCHES is not None:
+        _LAUNCHES.append(args[0] if fn is N.call else getattr(fn, "__name__", str(fn)))
     if _PROBE is None:
         return fn(*args)
     e0 = torch.cuda.Event(enable_timing=True)
@@ -168,6 +185,30 @@ def _launch(family, flops, fn, *args, tag=None, pieces=0):
 
 def conv_flops(B, H, W, cin, cout):
     return 2.0 * B * H * W * cin * cout * 9
+
+
+# ----------------------------------------------------------------------------- state record
+_RECORD = None
+
+
+@contextlib.contextmanager
+def record_state():
+    """Test hook: collects {layer name: (y, st)} -- the pre-norm conv output and InstanceNorm
+    statistics every conv block of a training forward saves for its backward -- of the
+    forwards run inside the block (the decision/state-pinned oracle of the parity tests,
+    oracle.vae_oracle.forward_from_state).  Holds references only; nothing is copied."""
+    global _RECORD
+    outer, rec = _RECORD, {}
+    _RECORD = rec
+    try:
+        yield rec
+    finally:
+        _RECORD = outer
+
+
+def _record(plan_layers, saved):
+    if _RECORD is not None:
+        _RECORD.update({L.name: saved[L.name] for L in plan_layers if L.name in saved})
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -620,6 +661,7 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True):
         if train:
             saved[L.name] = (y, st)
         src, sst = y, st
+    _record(plan.enc, saved)
     s, C = plan.enc_side, plan.enc_channels
     out = _empty(B, s, s, C, like=x)
     N.call("ebsdvae_act_apply", N.ptr(src), N.ptr(sst), ACT_NORM_POOL, N.ptr(out), B, s, s, C,
@@ -734,6 +776,7 @@ def decoder_forward(plan: Plan, dec_in, params, packs=None):
                              wp=_wp(packs, L.name, 0))
         saved[L.name] = (y, st)
         src, sst = y, st
+    _record(plan.dec, saved)
     S = plan.image_size
     x_hat = _empty(B, 1, S, S, like=dec_in)
     N.call("ebsdvae_conv3x3_cout1_fwd", N.ptr(src), N.ptr(sst), ACT_NORM,

@@ -675,3 +675,51 @@ def test_dgrad_summed_upsample_adjoint(cuda, cin, cout, H, prec):
     ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
     assert O.rel_err(host(g_prev), ref) < 2e-4
     assert O.rel_err(host(g_prev), host(g_prev2)) < 2e-4
+
+
+WG_F16_CASES = [  # (cin, cout, H, source mode, kind): NORM, NORM_UP and pooled-RAW sources
+    (32, 32, 128, E.ACT_NORM, 0), (32, 64, 64, E.ACT_NORM_POOL, 0), (64, 128, 32, E.ACT_NORM_POOL, 0),
+    (128, 64, 32, E.ACT_NORM, 1), (64, 32, 64, E.ACT_NORM, 1), (32, 32, 128, E.ACT_NORM_UP, 1),
+    (128, 128, 16, E.ACT_NORM_UP, 1), (64, 64, 64, E.ACT_NORM, 0),
+]
+
+
+@pytest.mark.parametrize("spread", [1.0, 1e3])
+@pytest.mark.parametrize("gscale", [1.0, 1e-7])
+@pytest.mark.parametrize("cin,cout,H,mode,kind", WG_F16_CASES)
+def test_conv_wgrad_f16(cuda, cin, cout, H, mode, kind, gscale, spread):
+    """Split-fp16 weight gradient (ebsdvae_conv3x3_wgrad_f16, the f16x3 default) == float64
+    oracle at 2e-5 norm-wise.  The gradient operand is scaled per slice by a power of two
+    from the per-tile maxima (gmax); gscale 1e-7 puts the unscaled gradient far below fp16's
+    normal range, and spread 1e3 makes the images of one slice 1e3 apart in magnitude
+    (one scale per slice from the largest)."""
+    if not N.call("ebsdvae_conv3x3_wgrad_split_slices", 2, H, H, cin, cout, E.PIECES_F16) > 0:
+        pytest.skip("shape not covered by the f16 weight gradient")
+    rng = np.random.default_rng(71 + cin + cout + H + mode)
+    B = 3 if H <= 64 else 2
+    s, mean, rstd, st = make_src(rng, B, H, cin, mode)
+    gy = rng.standard_normal((B, H, H, cout)) * gscale
+    gy[0] /= spread
+    wshape = (cout, cin, 3, 3) if kind == 0 else (cin, cout, 3, 3)
+    dw = torch.empty(wshape, device="cuda")
+    db = torch.empty(cout, device="cuda")
+    with E.precision("f16x3"):
+        g_d = dev(gy)
+        Tg = 4
+        g_d.ev_gmax = dev(np.abs(gy).reshape(B, Tg, -1).max(2))   # per-tile maxima (row bands)
+        if mode == E.ACT_NORM_POOL:
+            layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
+            wdummy = dev(np.zeros((cout, cin, 3, 3)))
+            _, _, act = E.conv_forward(dev(s), dev(st), layer, wdummy, dev(np.zeros(cout)), B, keep_act=True)
+            with E.record_launches() as launched:
+                E.conv_wgrad(act, None, E.ACT_RAW, g_d, cin, cout, kind, dw, db, normalized=True)
+        else:
+            with E.record_launches() as launched:
+                E.conv_wgrad(dev(s), dev(st), mode, g_d, cin, cout, kind, dw, db)
+    assert "ebsdvae_conv3x3_wgrad_f16" in launched
+    a = act_oracle(s, mean, rstd, mode)
+    rw, rb = O.conv3x3_wgrad(a, gy)
+    if kind == 1:
+        rw = rw.transpose(1, 0, 2, 3)[:, :, ::-1, ::-1]
+    assert O.rel_err(host(dw), rw) < SPLIT_TOL["f16x3"]
+    assert O.rel_err(host(db), rb) < 5e-5
