@@ -1,32 +1,58 @@
-"""On-device pattern ingest for the MI355X path (latice/data_module.py in the reference).
+"""Drop-in `latice.data_module` (reference: latice/data_module.py) with the pattern transform
+on the MI355X.
 
 The reference converts one pattern at a time on CPU DataLoader workers
-(`DPdataset.__getitem__`, data_module.py:125-133, through create_default_transform
-:17-33: ToPILImage -> Grayscale -> CenterCrop -> ToTensor).  Here a whole batch of raw
-patterns is copied to HBM once and transformed by one HIP launch
-(`ebsdvae_ingest_patterns`, csrc/ingest.hip), so the training step and
-build_dictionary are fed without a CPU stage per sample.
+(`DPdataset.__getitem__`, data_module.py:122-133, through `create_default_transform`
+:17-33: ToPILImage -> Grayscale -> CenterCrop -> ToTensor).  Here the same transform runs as
+one HIP launch over a whole batch (`ebsdvae_ingest_patterns`, csrc/ingest.hip: float -> x255
+-> uint8 cast, centre crop / zero pad, /255), fed from a memory-mapped .npy through pinned
+host buffers that a background thread fills while the GPU works.
 
-    ingest_patterns(raw (B, H0, W0) float64/float32, image_size) -> (B, 1, h, w) fp32 on device
-    DPdataset(path, rot_angles_path, image_size)   .npy memmap + angle file (data_module.py:36-133)
-        .batch(indices) -> (patterns on device, angles (B, 3) float64)
-        .iter_batches(batch_size) -> device batches in order (pinned host staging)
+Same public names, constructor arguments and behaviour as the reference:
 
-There is no CPU fallback: the transform runs on the ROCm device or raises.
+    create_default_transform(image_size)  -> callable: one (H, W) pattern -> (1, h, w) fp32
+    DPdataset(path, rot_angles_path, image_size, transform)   data_module.py:36-133
+    DPDataModule(path, rot_angles_path, image_size, val_data_ratio, batch_size, n_cpu,
+                 seed, transform)                             data_module.py:136-261
+        .setup(stage)   random_split(seed) for "fit", the whole set for "test" (:194-213)
+        .train_dataloader() / .val_dataloader() / .test_dataloader()
+            iterables of (patterns (B, 1, h, w) fp32 ON THE DEVICE, angles (B, 3) float64)
+            with len() = number of batches, as torch DataLoaders of the reference's
+            collated batches (callers' `data.to(device)` is then a no-op).
+
+Lightning is optional: DPDataModule subclasses `pl.LightningDataModule` when
+pytorch_lightning is importable.  There is no CPU fallback: the transform runs on the ROCm
+device or raises.  A user-supplied `transform` (any callable of the reference's kind) is
+honoured per pattern, exactly as the reference applies it.
 """
 from __future__ import annotations
 
 import logging
+import math
+import threading
 from pathlib import Path
 
 import numpy as np
 import torch
+from torch.utils.data import random_split
 
 from . import _native as N
+
+try:  # pragma: no cover - depends on the environment
+    import pytorch_lightning as pl
+    _DMBase = pl.LightningDataModule
+except Exception:  # noqa: BLE001
+    pl = None
+    _DMBase = object
 
 logger = logging.getLogger(__name__)
 
 _DTYPES = {torch.float64: 0, torch.float32: 1}
+
+
+def _default_device() -> torch.device:
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device("cuda")
 
 
 def ingest_patterns(raw, image_size=(128, 128), device="cuda", out: torch.Tensor | None = None):
@@ -50,48 +76,253 @@ def ingest_patterns(raw, image_size=(128, 128), device="cuda", out: torch.Tensor
     return out
 
 
+class PatternTransform:
+    """What `create_default_transform(image_size)` returns (data_module.py:17-33): called on
+    one pattern -- an (H, W) or (1, H, W) array or tensor -- it returns the (1, h, w) float32
+    tensor torchvision's ToPILImage -> Grayscale -> CenterCrop -> ToTensor would, computed on
+    the device.  `.batch(raw)` transforms a whole (B, H, W) stack in one launch."""
+
+    def __init__(self, image_size, device=None):
+        self.image_size = tuple(image_size) if not isinstance(image_size, int) else (image_size,) * 2
+        self.device = torch.device(device) if device is not None else None
+
+    def _dev(self):
+        return self.device if self.device is not None else _default_device()
+
+    def __call__(self, pattern):
+        t = torch.as_tensor(pattern)
+        if t.ndim == 3 and t.shape[0] == 1:
+            t = t[0]
+        if t.ndim != 2:
+            raise ValueError(f"expected one (H, W) pattern, got {tuple(t.shape)}")
+        return ingest_patterns(t, self.image_size, self._dev())[0]
+
+    def batch(self, raw):
+        return ingest_patterns(raw, self.image_size, self._dev())
+
+    def __repr__(self):
+        return f"PatternTransform(image_size={self.image_size}, device={self.device})"
+
+
+def create_default_transform(image_size: tuple[int, int]) -> PatternTransform:
+    """data_module.py:17-33 (ToPILImage -> Grayscale -> CenterCrop(image_size) -> ToTensor)."""
+    return PatternTransform(image_size)
+
+
 def parse_rotation_angles(rot_angles_path) -> np.ndarray:
     """data_module.py:87-116: skip two header lines, whitespace-split "z1 x z2" rows."""
-    with open(rot_angles_path) as f:
-        lines = f.readlines()[2:]
-    rows = [[a for a in line.strip().split(" ") if a] for line in lines]
-    return np.asarray(rows, dtype=float).reshape(-1, 3)
+    try:
+        with open(rot_angles_path) as f:
+            lines = f.readlines()[2:]
+        rows = [[a for a in line.strip().split(" ") if a] for line in lines]
+        return np.asarray(rows, dtype=float).reshape(-1, 3)
+    except FileNotFoundError:
+        logger.error(f"Rotation angles file not found: {rot_angles_path}")
+        raise
+    except Exception as e:  # noqa: BLE001
+        raise ValueError(f"Failed to parse rotation angles file: {e}") from e
 
 
 class DPdataset:
-    """data_module.py:36-133 with batched on-device transforms.  The pattern file is
-    memory-mapped (the reference loads it whole, :70)."""
+    """data_module.py:36-133.  The pattern file is memory-mapped (the reference loads it
+    whole, :70); `rot_angles` is the same pandas DataFrame (z1, x, z2).  Indexing returns
+    (transform(pattern) (1, h, w), angles (3,) float64) like the reference; `batch(indices)`
+    returns a whole device batch from one pinned copy and one transform launch."""
 
-    def __init__(self, path, rot_angles_path, image_size=(128, 128), device="cuda") -> None:
+    def __init__(self, path, rot_angles_path, image_size=(128, 128), transform=None,
+                 device=None) -> None:
         path = Path(path)
         try:
             self.ebsp_dataset = np.load(path, mmap_mode="r")
-        except Exception as e:
+            logger.info(f"Loaded diffraction pattern data from {path}")
+        except Exception as e:  # noqa: BLE001
             raise ValueError("Only .npy data files are supported.") from e
         if len(self.ebsp_dataset.shape) != 3:
             raise ValueError("The input dataset should be 3D.")
-        self.rot_angles = parse_rotation_angles(rot_angles_path)
+        self._angles = parse_rotation_angles(rot_angles_path)
         self.image_size = tuple(image_size)
-        self.device = torch.device(device)
+        self.transform = transform or create_default_transform(self.image_size)
+        self.device = torch.device(device) if device is not None else None
         self._pinned = None
+        self._pinned_free = None   # HIP event: the last device copy out of _pinned finished
+
+    @property
+    def rot_angles(self):
+        import pandas as pd
+        return pd.DataFrame(self._angles, columns=["z1", "x", "z2"])
 
     def __len__(self) -> int:
         return self.ebsp_dataset.shape[0]
 
+    def __getitem__(self, idx: int):
+        dp = np.asarray(self.ebsp_dataset[idx]).astype(np.float64)
+        return self.transform(dp), self._angles[idx].copy()
+
+    def _dev(self):
+        return self.device if self.device is not None else _default_device()
+
+    def load_raw(self, indices, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Raw patterns of `indices` (sorted runs read straight from the memmap) copied into
+        the host tensor `out` (pinned) or a new one."""
+        idx = np.asarray(indices, dtype=np.int64)
+        raw = self.ebsp_dataset[idx]
+        if raw.dtype not in (np.float64, np.float32):
+            raw = raw.astype(np.float64)
+        src = torch.from_numpy(np.ascontiguousarray(raw))
+        if out is None:
+            return src
+        dst = out[: src.numel()].view(src.shape)
+        dst.copy_(src)
+        return dst
+
+    def to_device(self, host_raw: torch.Tensor) -> torch.Tensor:
+        """(B, H0, W0) raw host batch -> (B, 1, h, w) fp32 device batch (DPdataset transform)."""
+        if isinstance(self.transform, PatternTransform):
+            return ingest_patterns(host_raw, self.image_size, self._dev())
+        # a user transform: applied per pattern, as the reference's __getitem__ does
+        return torch.stack([torch.as_tensor(self.transform(p.numpy().astype(np.float64)))
+                            for p in host_raw]).to(self._dev())
+
     def batch(self, indices):
         """(patterns (B, 1, h, w) fp32 on device, angles (B, 3) float64) for `indices`."""
         idx = np.asarray(indices, dtype=np.int64)
-        raw = np.ascontiguousarray(self.ebsp_dataset[idx])
-        if raw.dtype not in (np.float64, np.float32):
-            raw = raw.astype(np.float64)
-        host = torch.from_numpy(raw)
-        if self._pinned is None or self._pinned.numel() < host.numel() or self._pinned.dtype != host.dtype:
-            self._pinned = torch.empty(host.numel(), dtype=host.dtype).pin_memory()
-        staged = self._pinned[: host.numel()].view(host.shape)
-        staged.copy_(host)
-        x = ingest_patterns(staged, self.image_size, self.device)
-        return x, self.rot_angles[idx]
+        shape = (len(idx),) + tuple(self.ebsp_dataset.shape[1:])
+        n = int(np.prod(shape))
+        dt = torch.float32 if self.ebsp_dataset.dtype == np.float32 else torch.float64
+        if self._pinned_free is not None:
+            self._pinned_free.synchronize()   # the async copy of the previous batch read it
+        if self._pinned is None or self._pinned.numel() < n or self._pinned.dtype != dt:
+            self._pinned = torch.empty(n, dtype=dt).pin_memory()
+        x = self.to_device(self.load_raw(idx, self._pinned))
+        self._pinned_free = torch.cuda.Event()
+        self._pinned_free.record()
+        return x, self._angles[idx]
 
     def iter_batches(self, batch_size: int):
         for s in range(0, len(self), batch_size):
             yield self.batch(np.arange(s, min(s + batch_size, len(self))))
+
+
+class DeviceBatchLoader:
+    """The DataLoader of the drop-in DPDataModule: batches of (patterns on the device,
+    angles (B, 3) float64 tensor) over a subset of a DPdataset, in order or shuffled per
+    epoch (torch's default generator, as DataLoader(shuffle=True)).  A background thread
+    reads batch i+1 from the memmap into the second of two pinned buffers while batch i is
+    copied and transformed on the device; a buffer is refilled only after the device copy
+    out of it has completed (HIP event)."""
+
+    def __init__(self, dataset: DPdataset, indices, batch_size: int, shuffle: bool = False,
+                 drop_last: bool = False):
+        self.dataset = dataset
+        self.indices = np.asarray(indices, dtype=np.int64)
+        self.batch_size = int(batch_size)
+        self.shuffle = bool(shuffle)
+        self.drop_last = bool(drop_last)
+
+    def __len__(self) -> int:
+        n = len(self.indices)
+        return n // self.batch_size if self.drop_last else math.ceil(n / self.batch_size)
+
+    def _order(self):
+        if not self.shuffle:
+            return self.indices
+        return self.indices[torch.randperm(len(self.indices)).numpy()]
+
+    def __iter__(self):
+        order = self._order()
+        nb = len(self)
+        if nb == 0:
+            return
+        ds = self.dataset
+        shape = tuple(ds.ebsp_dataset.shape[1:])
+        dt = torch.float32 if ds.ebsp_dataset.dtype == np.float32 else torch.float64
+        per = int(np.prod(shape))
+        bufs = [torch.empty(self.batch_size * per, dtype=dt).pin_memory() for _ in range(2)]
+        done = [None, None]            # HIP event: device copy out of bufs[k] finished
+        ready = [threading.Event(), threading.Event()]
+        staged = [None, None]
+        err = []
+
+        def fill(i):
+            k = i & 1
+            try:
+                if done[k] is not None:
+                    done[k].synchronize()
+                sel = np.sort(order[i * self.batch_size:(i + 1) * self.batch_size])
+                staged[k] = (ds.load_raw(sel, bufs[k]), sel)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+            ready[k].set()
+
+        th = threading.Thread(target=fill, args=(0,), daemon=True)
+        th.start()
+        for i in range(nb):
+            k = i & 1
+            ready[k].wait()
+            th.join()
+            if err:
+                raise err[0]
+            ready[k].clear()
+            host, sel = staged[k]
+            x = ds.to_device(host)
+            ev = torch.cuda.Event()
+            ev.record()
+            done[k] = ev
+            if i + 1 < nb:
+                th = threading.Thread(target=fill, args=(i + 1,), daemon=True)
+                th.start()
+            yield x, torch.from_numpy(ds._angles[sel])
+
+
+class DPDataModule(_DMBase):
+    """data_module.py:136-261: same arguments, split and loaders; the loaders yield device
+    batches (DeviceBatchLoader).  `n_cpu` is accepted for API compatibility: there are no
+    worker processes (one transform launch per batch replaces them)."""
+
+    def __init__(self, path, rot_angles_path, image_size=(128, 128), val_data_ratio: float = 0.1,
+                 batch_size: int = 32, n_cpu: int = 4, seed: int = 42, transform=None,
+                 device=None):
+        super().__init__()
+        self.path = path
+        self.rot_angles_path = rot_angles_path
+        self.image_size = tuple(image_size)
+        self.val_data_ratio = val_data_ratio
+        self.batch_size = batch_size
+        self.n_cpu = n_cpu
+        self.seed = seed
+        self.transform = transform or create_default_transform(self.image_size)
+        torch.manual_seed(seed)          # data_module.py:184-186
+        np.random.seed(seed)
+        self.dataset_full = DPdataset(self.path, self.rot_angles_path, self.image_size,
+                                      self.transform, device=device)
+
+    def setup(self, stage: str | None = None) -> None:
+        """data_module.py:192-213 (random_split with a generator seeded by `seed`)."""
+        if stage == "fit" or stage is None:
+            all_size = len(self.dataset_full)
+            val_size = int(all_size * self.val_data_ratio)
+            train_size = all_size - val_size
+            logger.info(f"Splitting dataset: {train_size} training, {val_size} validation samples")
+            self.dataset_train, self.dataset_val = random_split(
+                self.dataset_full, [train_size, val_size],
+                generator=torch.Generator().manual_seed(self.seed))
+        if stage == "test":
+            self.dataset_test = self.dataset_full
+            logger.info(f"Test dataset prepared with {len(self.dataset_test)} samples")
+
+    def _loader(self, subset, shuffle):
+        idx = subset.indices if hasattr(subset, "indices") else np.arange(len(subset))
+        return DeviceBatchLoader(self.dataset_full, idx, self.batch_size, shuffle=shuffle)
+
+    def train_dataloader(self) -> DeviceBatchLoader:
+        """data_module.py:215-233 (with no validation split, the whole set)."""
+        if self.val_data_ratio > 0.0:
+            return self._loader(self.dataset_train, shuffle=True)
+        idx = np.concatenate([np.asarray(self.dataset_train.indices), np.asarray(self.dataset_val.indices)])
+        return DeviceBatchLoader(self.dataset_full, idx, self.batch_size, shuffle=True)
+
+    def val_dataloader(self) -> DeviceBatchLoader:
+        return self._loader(self.dataset_val, shuffle=False)
+
+    def test_dataloader(self) -> DeviceBatchLoader:
+        return self._loader(self.dataset_test, shuffle=False)

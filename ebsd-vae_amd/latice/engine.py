@@ -187,6 +187,21 @@ def conv_flops(B, H, W, cin, cout):
     return 2.0 * B * H * W * cin * cout * 9
 
 
+# ----------------------------------------------------------------------------- weight writes
+# Kernels that update parameters through raw pointers (the fused Adam) bypass torch's
+# version counters; they bump this generation so cached weight packs are refreshed.
+_WEIGHTS_GEN = 0
+
+
+def weights_written() -> None:
+    global _WEIGHTS_GEN
+    _WEIGHTS_GEN += 1
+
+
+def weights_generation() -> int:
+    return _WEIGHTS_GEN
+
+
 # ----------------------------------------------------------------------------- state record
 _RECORD = None
 

@@ -13,11 +13,17 @@ fallback: the model must live on a ROCm device (model.to("cuda")).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from . import engine as E
+from .deferred import DeferredTensor
 from .functional import DecoderFn, EncoderFn, HeadsFn, LinearFn, ReparamFn
+
+# EBSDVAE_DEFER_DECODE=0: the eval/no-grad forward runs the decoder eagerly (A/B timing)
+_DEFER = os.environ.get("EBSDVAE_DEFER_DECODE", "1") != "0"
 
 
 def _draw_eps(shape, device) -> torch.Tensor:
@@ -89,7 +95,15 @@ class VariationalAutoEncoder(nn.Module):
 
     def forward(self, x: torch.Tensor, eps: torch.Tensor | None = None):
         """Returns (z, x_hat, mu, std) like latice/model.py:40-66.  `eps` (B, latent) may be
-        supplied to make the reparameterisation noise deterministic (parity tests)."""
+        supplied to make the reparameterisation noise deterministic (parity tests).
+
+        In eval mode with autograd off (build_dictionary, encode_pattern(s), validation)
+        x_hat comes back as a DeferredTensor: the decoder runs only if x_hat is used, so
+        `_, _, mu, _ = model(data)` (latice/index/dp_indexer.py:136,183,284) costs the
+        encoder and the heads alone -- one model call per batch, as the reference's callers
+        and tests expect (tests/index/test_dp_indexer.py:305)."""
+        if _DEFER and not self.training and not torch.is_grad_enabled():
+            return self._forward_inference(x, eps)
         enc = self.encoder(x)
         if eps is None:
             eps = _draw_eps((x.shape[0], self.mu[0].out_features), x.device)
@@ -99,6 +113,44 @@ class VariationalAutoEncoder(nn.Module):
         x_hat = self.decoder(dec_in)
         return z, x_hat, mu, std
 
+    def _inference_packs(self, params):
+        """Packed conv weights for inference launches, repacked only when a parameter changed
+        (storage or version counter) or the conv arithmetic was switched."""
+        key = (E.get_precision(), E.weights_generation()) + tuple(
+            (p.data_ptr(), p._version) for p in params.values())
+        cached = getattr(self, "_packcache", None)
+        if cached is None or cached[0] != key:
+            ps = E.PackSet(self._plan, params)
+            cached = (key, ps, ps.refresh())
+            object.__setattr__(self, "_packcache", cached)
+        return cached[2]
+
+    def _forward_inference(self, x, eps):
+        if x.device.type != "cuda":
+            raise RuntimeError("the HIP VAE needs a ROCm device tensor (no CPU fallback)")
+        plan = self._plan
+        x = x.float().contiguous()
+        params = dict(self.named_parameters())
+        packs = self._inference_packs(params)
+        enc, _ = E.encoder_forward(plan, x, params, packs=packs, train=False)
+        if eps is None:
+            eps = _draw_eps((x.shape[0], plan.latent_dim), x.device)
+        _, mu, std, z, dec_in = E.heads_forward(plan, enc, params, eps.float().contiguous())
+        versions = [(p, p._version) for p in params.values()]
+        gen = E.weights_generation()
+
+        def decode():
+            if gen != E.weights_generation() or any(p._version != v for p, v in versions):
+                raise RuntimeError("model parameters changed between model(x) and the first use "
+                                   "of its deferred x_hat")
+            with torch.no_grad():
+                x_hat, _ = E.decoder_forward(plan, dec_in, params,
+                                             packs=self._inference_packs(params))
+            return x_hat
+
+        S = plan.image_size
+        return z, DeferredTensor(decode, (x.shape[0], 1, S, S), torch.float32, x.device), mu, std
+
     @torch.no_grad()
     def encode_mu(self, x: torch.Tensor) -> torch.Tensor:
         """Encoder-only fast path: mu == forward(x)[2] (the only output
@@ -107,7 +159,8 @@ class VariationalAutoEncoder(nn.Module):
         if x.device.type != "cuda":
             raise RuntimeError("encode_mu needs a ROCm device tensor (no CPU fallback)")
         params = dict(self.named_parameters())
-        return E.encode_latents(self._plan, x.contiguous(), params)
+        return E.encode_latents(self._plan, x.float().contiguous(), params,
+                                packs=self._inference_packs(params))
 
     @staticmethod
     def weights_init(m: nn.Module) -> None:

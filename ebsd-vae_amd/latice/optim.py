@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as N
+from . import engine as E
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -48,4 +49,5 @@ class FusedAdam(torch.optim.Optimizer):
                        N.ptr(st["exp_avg_sq"]), N.ptr(st.get("max_exp_avg_sq")), N.ptr(st["step"]),
                        p.numel(), float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                        float(group["weight_decay"]), int(bool(group["amsgrad"])), N.stream())
+        E.weights_written()
         return loss

@@ -137,6 +137,7 @@ class VAETrainer:
                N.ptr(self.exp_avg_sq), N.ptr(self.max_exp_avg_sq), N.ptr(self.step_count),
                self.flat.numel(), self.lr, float(b1), float(b2), self.adam_eps, self.weight_decay,
                int(self.amsgrad), N.stream())
+        E.weights_written()
 
     def step(self, x: torch.Tensor, eps: torch.Tensor | None = None):
         out = self.forward_backward(x, eps)
@@ -163,4 +164,5 @@ class VAETrainer:
 
     def replay(self):
         self.graph.replay()
+        E.weights_written()
         return self._static[1]

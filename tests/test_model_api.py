@@ -77,3 +77,41 @@ def test_lightning_module_api():
     assert sched is not None
     cfg = lm.configure_optimizers()
     assert set(cfg) == {"optimizer", "lr_scheduler", "monitor"}
+
+
+def test_deferred_tensor_computes_on_first_use_only():
+    """latice.deferred.DeferredTensor (the eval/no-grad x_hat): metadata without running
+    the thunk; any value access runs it once; results are plain tensors."""
+    from latice.deferred import DeferredTensor
+    calls = []
+
+    def thunk():
+        calls.append(1)
+        return torch.arange(6.0).reshape(2, 1, 3)
+
+    d = DeferredTensor(thunk, (2, 1, 3), torch.float32, torch.device("cpu"))
+    assert d.shape == (2, 1, 3) and d.dim() == 3 and d.dtype == torch.float32 and len(d) == 2
+    assert d.numel() == 6 and not d.requires_grad and not d.materialized and calls == []
+    assert type(d * 2) is torch.Tensor and float((d * 2).sum()) == 30.0
+    assert d.numpy().tolist() == [[[0.0, 1.0, 2.0]], [[3.0, 4.0, 5.0]]]
+    assert torch.equal(torch.sigmoid(d), torch.sigmoid(torch.arange(6.0).reshape(2, 1, 3)))
+    assert calls == [1] and d.materialized
+    bad = DeferredTensor(lambda: torch.zeros(3), (2,), torch.float32, torch.device("cpu"))
+    with pytest.raises(RuntimeError, match="does not match"):
+        bad.sum()
+
+
+def test_datamodule_split_matches_random_split(tmp_path):
+    """DPDataModule.setup('fit') splits exactly like the reference's random_split with the
+    seeded generator (latice/data_module.py:194-207); loaders report len() in batches."""
+    import numpy as np
+    from latice.data_module import DPDataModule
+    np.save(tmp_path / "p.npy", np.zeros((23, 130, 130)))
+    with open(tmp_path / "a.txt", "w") as f:
+        f.write("eu\n23\n" + "".join(f"{i} {i} {i}\n" for i in range(23)))
+    dm = DPDataModule(tmp_path / "p.npy", tmp_path / "a.txt", batch_size=4, val_data_ratio=0.25, seed=7)
+    dm.setup("fit")
+    perm = torch.randperm(23, generator=torch.Generator().manual_seed(7)).tolist()
+    assert list(dm.dataset_train.indices) == perm[:18] and list(dm.dataset_val.indices) == perm[18:]
+    assert len(dm.train_dataloader()) == 5 and len(dm.val_dataloader()) == 2
+    assert list(dm.dataset_full.rot_angles.columns) == ["z1", "x", "z2"]
