@@ -11,11 +11,17 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus:
   roofline      the dominant kernel family (by GPU time), its algorithmic FLOPs per
                 launch / average launch duration (HIP events on the launch stream, live in
                 the timed region on every --probe-every'th step) against the peak of the
-                conv arithmetic (bf16 MFMA / products per fp32 product, or fp32 MFMA);
+                conv arithmetic (fp16/bf16 MFMA / products per fp32 product, or fp32 MFMA);
+                roofline.step: the attainable-roofline fraction of the whole step,
+                sum_k max(F_k / P_k, B_k / BW) / T (SURVEY.md section 8d);
+  strict_fp32   the same step with every conv on v_mfma_f32 (no split arithmetic);
   c5_256        the c5 configuration (256x256, latent 64, batch 128/GPU) step rate;
-  c4_encoder_latents  build_dictionary throughput and a batched query;
+  c4_encoder_latents  build_dictionary throughput through the unmodified
+                DiffractionPatternIndexer loop (one model(x) call per batch, mu kept) and a
+                batched query;
   cpu_baseline  oracle/torch_port.py (PyTorch-CPU restatement of the reference
-                training_step) timed on this host's cores on a bounded sample (N=1, rank 0).
+                training_step) on this host's cores, at BASELINE.md section 4's shapes
+                (B=8, B=256, encoder-only B=1024; N=1, rank 0).
 """
 from __future__ import annotations
 
@@ -69,98 +75,156 @@ def pmc_traffic(fam: str):
         return None
 
 
-def cpu_baseline(plan, seconds: float, batch: int):
+def _cpu_name():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(plan, timed: int = 3):
+    """the PyTorch-CPU restatement of the reference training step
+    (oracle/torch_port.py, parity-pinned to the reference's golden vectors) on all of this
+    rank's host cores: B=8 (c1), B=256 (c2's shape) fwd+loss+bwd+Adam and encoder+mu at
+    B=1024 (c4), each 1 warm-up + the median of `timed` steps.  value = the B=256 rate."""
     from latice.seeding import seeded_state_dict, synthetic_patterns
     from oracle.torch_port import CPUStep   # oracle: the baseline leg only
+    # the box's CPU share: OMP_NUM_THREADS when set (the affinity mask can list every CPU of
+    # the machine while the job's quota is far smaller: oversubscribing it is 10x slower)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
     sd = seeded_state_dict(0, plan.inplanes, plan.latent_dim, plan.image_size)
+    S, L = plan.image_size, plan.latent_dim
+
+    def median_rate(fn, batch):
+        log(f"[bench] cpu baseline: batch {batch} on {threads} threads")
+        x = torch.from_numpy(synthetic_patterns(123, batch, S))
+        eps = torch.randn(batch, L)
+        fn(x[: min(batch, 8)], eps[: min(batch, 8)])     # warm-up (allocator, oneDNN)
+        ts = []
+        for _ in range(timed):
+            t0 = time.perf_counter()
+            fn(x, eps)
+            ts.append(time.perf_counter() - t0)
+            log(f"[bench]   {ts[-1]:.2f} s")
+        return batch / float(np.median(ts)), float(np.median(ts))
+
     st = CPUStep(sd, kl_lambda=5e-6)
-    x = torch.from_numpy(synthetic_patterns(123, batch, plan.image_size))
-    eps = torch.randn(batch, plan.latent_dim)
-    st.step(x, eps)                     # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        st.step(x, eps)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 50:
-            break
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": round(n * batch / el, 3), "unit": "patterns/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} timed steps (+1 warm-up) of fwd+loss+bwd+Adam at batch {batch}, "
-                      f"{plan.image_size}x{plan.image_size}, PyTorch-CPU restatement "
-                      f"(oracle/torch_port.py), {threads} threads, {cpu}"}
+    r8, t8 = median_rate(st.step, 8)
+    r256, t256 = median_rate(st.step, 256)
+    renc, tenc = median_rate(lambda x, e: st.encode(x), 1024)
+    return {"value": round(r256, 3), "unit": "patterns/s", "cores": threads, "kind": "port",
+            "sample": f"median of {timed} timed steps (after a warm-up) of fwd+loss+bwd+Adam at batch "
+                      f"256, {S}x{S}, PyTorch-CPU restatement of the reference training_step "
+                      f"(oracle/torch_port.py), {threads} threads, {_cpu_name()}",
+            "b8_patterns_per_s": round(r8, 3), "b8_s_per_step": round(t8, 4),
+            "b256_s_per_step": round(t256, 3),
+            "encoder_b1024_latents_per_s": round(renc, 2), "encoder_b1024_s_per_batch": round(tenc, 3)}
+
+
+class _SyntheticPatternLoader:
+    """A DPDataModule test_dataloader stand-in over synthetic raw patterns already in HBM:
+    each batch is the on-device DPdataset transform (ebsdvae_ingest_patterns) of a raw
+    float64 batch, with its angles -- what build_dictionary's loop consumes."""
+
+    def __init__(self, raw, image_size, nb, angles):
+        from latice.data_module import ingest_patterns
+        self._ingest = ingest_patterns
+        self.raw, self.S, self.nb, self.angles = raw, image_size, nb, angles
+        self.x = torch.empty(raw.shape[0], 1, image_size, image_size, dtype=torch.float32,
+                             device=raw.device)
+
+    def __len__(self):
+        return self.nb
+
+    def __iter__(self):
+        B = self.raw.shape[0]
+        for i in range(self.nb):
+            yield (self._ingest(self.raw, (self.S, self.S), out=self.x),
+                   torch.from_numpy(self.angles[i * B:(i + 1) * B]))
 
 
 def encoder_latents(model, plan, args, dev, world):
     """BASELINE c4: DiffractionPatternIndexer.build_dictionary (latice/index/dp_indexer.py:
-    92-111, 254-297) end to end on the device, at batch 1024 per GPU: raw float64 patterns
-    (synthetic, already in HBM) -> the DPdataset transform (ebsdvae_ingest_patterns) ->
-    encoder + mu head (encode_latents) -> L2-normalised rows appended to the HBM dictionary
-    (latice.index.faiss_db).  c4_batches (default 1024 = 1,048,576 patterns) are split over
-    the ranks; no collective.  Then one batched query of 4096 latents against the dictionary:
-    cosine top-20 + orientation consensus (faiss_db.find_best_orientations_batch)."""
-    from latice import engine as E
-    from latice.data_module import ingest_patterns
-    from latice.index.faiss_db import FaissLatentVectorDatabase, FaissLatentVectorDatabaseConfig
+    92-111, 254-297) at batch 1024 per GPU through the UNMODIFIED loop of the drop-in
+    indexer: per batch the on-device transform, ONE `self.model(data)` call whose `[2]` is
+    kept (the model's eval/no-grad forward defers the decoder, so it runs encoder + heads),
+    `mu.cpu().numpy()`; then `db.add_vectors` into the HBM dictionary.  c4_batches (default
+    1024 = 1,048,576 patterns) are split over the ranks; no collective.  Then one batched
+    query of 4096 latents: cosine top-20 + orientation consensus."""
+    import contextlib
     import logging
+    from latice import engine as E
+    from latice.index.dp_indexer import DiffractionPatternIndexer, IndexerConfig
+    from latice.index.faiss_db import FaissLatentVectorDatabase, FaissLatentVectorDatabaseConfig
     logging.getLogger("latice.index.faiss_db").setLevel(logging.ERROR)   # random angles never agree
     B, S = 1024, args.image_size
     H0 = S + 12   # raw patterns a little larger than the crop, as in the reference pipeline
     nb = max(1, args.c4_batches // world)
-    params = dict(model.named_parameters())
     gen = torch.Generator(device=dev).manual_seed(7 + dist.get_rank() if world > 1 else 7)
     raw = torch.rand(B, H0, H0, dtype=torch.float64, device=dev, generator=gen)
     angles = np.random.default_rng(11).uniform(0.0, 360.0, (nb * B, 3))
-    x = torch.empty(B, 1, S, S, dtype=torch.float32, device=dev)
-    packs = E.PackSet(plan, params).refresh()
     db = FaissLatentVectorDatabase(FaissLatentVectorDatabaseConfig(
         npz_path="/nonexistent/c4_dictionary.npz", dimension=plan.latent_dim, device=str(dev)))
     db.reserve(nb * B)
+    cfg = IndexerConfig(pattern_path="/nonexistent/patterns.npy", angles_path="/nonexistent/angles.txt",
+                        batch_size=B, device="cuda", latent_dim=plan.latent_dim, image_size=(S, S))
+    ix = DiffractionPatternIndexer(model, db=db, config=cfg)
+    quiet = contextlib.redirect_stdout(sys.stderr)   # the indexer's progress bar
+    with quiet:
+        ix._extract_latent_vectors_with_angles(_SyntheticPatternLoader(raw, S, 2, angles))  # warm-up
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with quiet:
+        lat, ori = ix._extract_latent_vectors_with_angles(_SyntheticPatternLoader(raw, S, nb, angles))
+        ix.db.add_vectors(lat, ori)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    finite = bool(np.isfinite(lat).all())
+    # the encoder-only engine loop without the per-batch host copy, for comparison
+    params = dict(model.named_parameters())
+    packs = model._inference_packs(params)
+    x = torch.empty(B, 1, S, S, dtype=torch.float32, device=dev)
+    ne = min(nb, 64)
     with torch.no_grad():
-        for _ in range(2):
-            E.encode_latents(plan, ingest_patterns(raw, (S, S), out=x), params, packs)
-        if world > 1:
-            dist.barrier()
+        from latice.data_module import ingest_patterns
+        E.encode_latents(plan, ingest_patterns(raw, (S, S), out=x), params, packs)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(nb):
+        t1 = time.perf_counter()
+        for _ in range(ne):
             mu = E.encode_latents(plan, ingest_patterns(raw, (S, S), out=x), params, packs)
-            db.add_vectors(mu, angles[i * B:(i + 1) * B])
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        finite = bool(torch.isfinite(mu).all())
+        eng = time.perf_counter() - t1
         # query leg: 4096 perturbed latents, top-20 + consensus over the whole dictionary
         q = (mu.repeat(4, 1) + 0.01 * torch.randn(4 * B, plan.latent_dim, device=dev, generator=gen))
         db.find_best_orientations_batch(q[:64], top_n=20)   # warm-up
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
+        t2 = time.perf_counter()
         res = db.find_best_orientations_batch(q, top_n=20)
         torch.cuda.synchronize()
-        qel = time.perf_counter() - t1
+        qel = time.perf_counter() - t2
     if world > 1:
-        t = torch.tensor([el, qel], device=dev, dtype=torch.float64)
+        t = torch.tensor([el, qel, eng], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, qel = float(t[0]), float(t[1])
+        el, qel, eng = float(t[0]), float(t[1]), float(t[2])
     n = world * B * nb
     enc_flops = sum(2.0 * L.H * L.H * L.cin * L.cout * 9 for L in plan.enc) + 2 * plan.feat * plan.latent_dim
-    return {"metric": "encoder latents/sec (c4: build_dictionary = ingest + encoder + mu head + "
-                      "dictionary add, batch 1024/GPU)",
+    return {"metric": "encoder latents/sec (c4: DiffractionPatternIndexer.build_dictionary loop = "
+                      "on-device transform + model(x)[2] + mu.cpu() per batch + dictionary add, "
+                      "batch 1024/GPU)",
             "value": round(n / el, 1), "unit": "latents/s", "latents": n,
             "ms_per_batch": round(el / nb * 1e3, 3),
             "tflops": round(enc_flops * n / el / 1e12, 2), "finite": finite,
+            "engine_only": {"value": round(world * B * ne / eng, 1), "unit": "latents/s",
+                            "batches": ne, "what": "transform + encode_latents, no host copy"},
             "query": {"metric": "queries/sec (cosine top-20 over the dictionary + orientation "
                                 "consensus, one batch per GPU)",
                       "value": round(world * len(res) / qel, 1), "unit": "queries/s",
@@ -208,6 +272,67 @@ def c5_step_rate(args, dev, world, rank):
             "step_fp32_tflops": round(step_tflops, 2), "loss_finite": bool(np.isfinite(loss))}
 
 
+def step_roofline(probe, plan, B, ms, probed, nparams):
+    """T_roof = sum_k max(F_k / P_k, B_k / BW) over the kernels of one
+    step, divided by the measured step time.  Conv launches (fwd, input gradient, weight
+    gradient) come from the probe with their algorithmic FLOPs, the peak of the arithmetic
+    they ran in and their algorithmic I/O bytes; the HBM-bound rest of the fused step is
+    counted by its algorithmic bytes: the final conv(32->1) forward and its fused backward
+    (read the 32-channel input twice + logits / logit gradient), the first block's fused
+    backward (read x), BCE+KL (read x_hat, x; write the logit gradient) and Adam (7 fp32
+    streams over the flat parameters).  Also given against the strict fp32 peak (every
+    conv at 157.3 TFLOP/s), the reading SURVEY.md section 8d states."""
+    from latice.engine import conv_flops
+    S = plan.image_size
+    bw = HBM_PEAK_GBS * 1e9
+    conv_s = probe.attainable_s(bw) / probed
+    conv_fp32_s = sum(max(f / (FP32_PEAK_TFLOPS * 1e12), nb / bw)
+                      for _, f, _, _, _, _, nb in probe.records) / probed
+    px = B * S * S
+    fin_f = conv_flops(B, S, S, plan.inplanes, 1)
+    rest = [(fin_f, 4.0 * px * (plan.inplanes + 1)),            # final conv forward
+            (2 * fin_f, 4.0 * px * (2 * plan.inplanes + 1)),     # its fused backward
+            (0.0, 4.0 * px),                                      # first block: read x
+            (0.0, 3 * 4.0 * px),                                  # BCE + KL fwd/bwd
+            (0.0, 28.0 * nparams)]                                # Adam
+    rest_s = sum(max(f / (FP32_PEAK_TFLOPS * 1e12), b / bw) for f, b in rest)
+    t = ms / 1e3
+    return {"definition": "sum_k max(F_k/P_k, B_k/BW) / T_step (SURVEY.md 8d)",
+            "attainable_ms": round((conv_s + rest_s) * 1e3, 3), "measured_ms": round(ms, 3),
+            "frac": round((conv_s + rest_s) / t, 4),
+            "frac_vs_fp32_peak": round((conv_fp32_s + rest_s) / t, 4),
+            "conv_attainable_ms": round(conv_s * 1e3, 3), "other_attainable_ms": round(rest_s * 1e3, 3)}
+
+
+def strict_fp32_rate(model, x, args, dev, world):
+    """The same training step with every conv on v_mfma_f32_32x32x2_f32 (no split
+    arithmetic), timed like the headline line (barrier + synchronize, max over ranks)."""
+    from latice import engine as E
+    from latice.trainer import VAETrainer
+    with E.precision("fp32"):
+        tr = VAETrainer(model, kl_lambda=5e-6, lr=1e-4, seed=3000)
+        for _ in range(2):
+            tr.step(x)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.strict_fp32_steps):
+            tr.step(x)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    del tr
+    return {"value": round(world * x.shape[0] * args.strict_fp32_steps / el, 2), "unit": "patterns/s",
+            "ms_per_step": round(el / args.strict_fp32_steps * 1e3, 3), "steps": args.strict_fp32_steps,
+            "dtype": "fp32"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -216,8 +341,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="patterns per GPU")
     ap.add_argument("--image-size", type=int, default=128)
     ap.add_argument("--latent-dim", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-batch", type=int, default=16)
+    ap.add_argument("--cpu-timed", type=int, default=3, help="timed CPU-baseline steps per shape")
+    ap.add_argument("--strict-fp32-steps", type=int, default=8,
+                    help="timed steps of the strict fp32-MFMA leg (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
     ap.add_argument("--probe-every", type=int, default=5,
@@ -315,22 +441,31 @@ def main():
                 "avg_launch_us": round(avg_s * 1e6, 2),
                 "gflop_per_launch": round(flops_per_launch / 1e9, 3),
                 "flops": "algorithmic fp32-equivalent (2*B*H*W*Cin*Cout*9 per conv)"}
+        roof["step"] = step_roofline(probe, plan, args.batch, ms, probed, trainer.numel)
     step_tflops = step_flops_per_pattern(plan) * args.batch / (ms / 1e3) / 1e12
 
+    prec = E.get_precision()
     res = {
         "metric": "EBSD patterns/sec (128x128, fwd+bwd)" if args.image_size == 128
         else f"EBSD patterns/sec ({args.image_size}x{args.image_size}, fwd+bwd)",
         "value": round(value, 2), "unit": "patterns/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-        "conv_arithmetic": E.get_precision() + {
-            "fp32": " (v_mfma_f32_32x32x2_f32)",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": {"fp32": "fp32", "bf16x6": "fp32 I/O, bf16x6 split MFMA",
+                  "bf16x3": "fp32 I/O, bf16x3 split MFMA",
+                  "f16x3": "fp32 I/O, f16x3 split MFMA"}[prec],
+        "data": "synthetic",
+        "conv_arithmetic": prec + {
+            "fp32": " (v_mfma_f32_32x32x2_f32 everywhere)",
             "bf16x6": " (fp32 operands split into 3 bf16 pieces, 6 bf16 MFMA products per fp32"
-                      " product, fp32 accumulation: fp32-grade, same parity gates as fp32)",
+                      " product, fp32 accumulation)",
             "bf16x3": " (2 bf16 pieces, 3 products: ~2^-16.5 per product)",
-            "f16x3": " (forward convs: fp32 operands split into 2 fp16 pieces, weights x256, 3 fp16"
-                     " MFMA products, ~2^-22.5 per product; input/weight gradients bf16x6; same"
-                     " parity gates as fp32)"}[E.get_precision()],
+            "f16x3": " (fp32 operands split into 2 fp16 pieces, 3 fp16 MFMA products per fp32"
+                     " product, ~2^-22.5, fp32 accumulation: forward convs with weights packed x256;"
+                     " input-gradient and weight-gradient convs with the gradient operand scaled"
+                     " by a power of two per image / per slice; fp32 MFMA for the 1->32 and 8x8"
+                     " layers where f16 is not supported; all activations, statistics and"
+                     " reductions fp32/fp64; passes the fp32 parity gates, tests/test_gpu_trainer.py)"}[prec],
         "config": {"workload": f"c{2 if world == 1 else 3}: VariationalAutoEncoderRawData "
                                f"{args.image_size}x{args.image_size}, latent {args.latent_dim}, "
                                f"batch {args.batch}/GPU, fwd+loss+bwd+Adam"
@@ -343,13 +478,15 @@ def main():
         "loss": round(loss, 6),
         "kernel_families_ms_per_step": {k: round(v["ms"] / max(1, probed), 3) for k, v in fam.items()},
     }
+    if args.strict_fp32_steps > 0:
+        res["strict_fp32"] = strict_fp32_rate(model, x, args, dev, world)
     if args.c5_steps > 0 and args.image_size == 128:
         res["c5_256"] = c5_step_rate(args, dev, world, rank)
     if args.c4_batches > 0:
         res["c4_encoder_latents"] = encoder_latents(model, plan, args, dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline ...")
-        res["cpu_baseline"] = cpu_baseline(plan, args.cpu_seconds, args.cpu_batch)
+        res["cpu_baseline"] = cpu_baseline(plan, args.cpu_timed)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

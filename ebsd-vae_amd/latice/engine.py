@@ -123,17 +123,24 @@ class probe:
         """{tag: [launches, flops, ms]} (per-layer view for tools/layer_profile.py)."""
         torch.cuda.synchronize()
         out = {}
-        for fam, flops, e0, e1, tag, _ in self.records:
+        for fam, flops, e0, e1, tag, _, _ in self.records:
             d = out.setdefault(f"{fam} {tag}", [0, 0.0, 0.0])
             d[0] += 1
             d[1] += flops
             d[2] += e0.elapsed_time(e1)
         return out
 
+    def attainable_s(self, hbm_bytes_per_s: float = 8e12) -> float:
+        """Sum over the recorded launches of max(F_k / P_k, B_k / BW): the attainable-roofline
+        time of these kernels, F_k the algorithmic fp32-equivalent
+        FLOPs, P_k the peak of the launch's arithmetic, B_k its algorithmic I/O bytes."""
+        return sum(max(flops / (mfma_peak(pieces) * 1e12), nb / hbm_bytes_per_s)
+                   for _, flops, _, _, _, pieces, nb in self.records)
+
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for fam, flops, e0, e1, _, pieces in self.records:
+        for fam, flops, e0, e1, _, pieces, _ in self.records:
             d = out.setdefault(fam, {"launches": 0, "flops": 0.0, "ms": 0.0, "peak_s": 0.0,
                                      "split_launches": 0})
             d["launches"] += 1
@@ -169,7 +176,7 @@ def record_launches():
         _LAUNCHES = outer
 
 
-def _launch(family, flops, fn, *args, tag=None, pieces=0):
+def _launch(family, flops, fn, *args, tag=None, pieces=0, nbytes=0):
     if _LAUNCHES is not None:
         _LAUNCHES.append(args[0] if fn is N.call else getattr(fn, "__name__", str(fn)))
     if _PROBE is None:
@@ -179,7 +186,7 @@ def _launch(family, flops, fn, *args, tag=None, pieces=0):
     e0.record()
     r = fn(*args)
     e1.record()
-    _PROBE.append((family, float(flops), e0, e1, tag, pieces))
+    _PROBE.append((family, float(flops), e0, e1, tag, pieces, float(nbytes)))
     return r
 
 
@@ -391,18 +398,20 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     args = (N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y),
             N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout)
     flops = conv_flops(B, H, H, layer.cin, layer.cout)
+    nb = 4 * (src.numel() + y.numel() + (y.numel() // 4 if pool_out else 0))   # algorithmic I/O
     ypool = None
     if pool_out:
         ypool = _empty(B, H // 2, H // 2, layer.cout, like=w)
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split_pooled", N.ptr(src),
                 N.ptr(src_stats), src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y), N.ptr(ypool),
                 N.ptr(part), B, H, H, layer.cin, layer.cout, wp.pieces, N.stream(), tag=tag + " pool",
-                pieces=wp.pieces)
+                pieces=wp.pieces, nbytes=nb)
     elif wp.pieces:
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split", *args, wp.pieces,
-                N.stream(), tag=tag, pieces=wp.pieces)
+                N.stream(), tag=tag, pieces=wp.pieces, nbytes=nb)
     else:
-        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", *args, N.stream(), tag=tag)
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", *args, N.stream(), tag=tag,
+                nbytes=nb)
     st = _empty(B, layer.cout, 2, like=w)
     N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
            N.stream())
@@ -533,6 +542,7 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
     if normalized is None:
         normalized = src_mode in (ACT_NORM, ACT_NORM_UP)
     gmax = getattr(gy, "ev_gmax", None)
+    nbw = 4 * (src.numel() + gy.numel())   # algorithmic I/O: source activation + gradient
     if (gmax is not None and normalized and _FWD_PIECES.get(_PRECISION)
             and os.environ.get("EBSDVAE_WGRAD_F16", "1") != "0"):
         S_ = N.call("ebsdvae_conv3x3_wgrad_split_slices", B, H, W, cin, cout, PIECES_F16)
@@ -543,7 +553,7 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
                     "ebsdvae_conv3x3_wgrad_f16", N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(gy),
                     N.ptr(gmax), gmax.shape[1], N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout,
                     N.stream(), tag=f"wgrad {cin:3d}->{cout:3d} @{H:3d} m{src_mode} f16",
-                    pieces=PIECES_F16)
+                    pieces=PIECES_F16, nbytes=nbw)
             _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
             return
     np_ = _PIECES[_PRECISION]
@@ -561,10 +571,10 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
     tag = f"wgrad {cin:3d}->{cout:3d} @{H:3d} m{src_mode}"
     if np_:
         _launch("conv3x3_wgrad", conv_flops(B, H, W, cin, cout), N.call, "ebsdvae_conv3x3_wgrad_split",
-                *args, np_, s, tag=tag, pieces=np_)
+                *args, np_, s, tag=tag, pieces=np_, nbytes=nbw)
     else:
         _launch("conv3x3_wgrad", conv_flops(B, H, W, cin, cout), N.call, "ebsdvae_conv3x3_wgrad",
-                *args, s, tag=tag)
+                *args, s, tag=tag, nbytes=nbw)
     _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
 
 
@@ -587,6 +597,7 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
         gin = _empty(B, H, W, layer.cin, like=gy)
     tag = f"dgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d}"
     flops = conv_flops(B, H, W, layer.cin, layer.cout)
+    nbd = 4 * (gy.numel() + gin.numel())   # algorithmic I/O: output gradient in, input gradient out
     if wd.pieces == PIECES_F16:
         gmax = getattr(gy, "ev_gmax", None)
         if gmax is None:
@@ -604,17 +615,17 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_f16", N.ptr(gy),
                 N.ptr(gmax), gmax.shape[1], N.ptr(wd.t), N.ptr(gin), yp, sp, pmode, pptr, B, H, W,
                 layer.cout, layer.cin, N.stream(), tag=tag + ("" if prev is None else " +inbwd"),
-                pieces=wd.pieces)
+                pieces=wd.pieces, nbytes=nbd)
         return gin if prev is None else (gin, part)
     if prev is None:
         if wd.pieces:
             _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_split", N.ptr(gy),
                     N.ptr(wd.t), N.ptr(gin), None, None, -1, None, B, H, W, layer.cout, layer.cin,
-                    wd.pieces, N.stream(), tag=tag, pieces=wd.pieces)
+                    wd.pieces, N.stream(), tag=tag, pieces=wd.pieces, nbytes=nbd)
         else:
             _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", N.ptr(gy), None, ACT_RAW,
                     N.ptr(wd.t), None, N.ptr(gin), None, None, B, H, W, layer.cout, layer.cin,
-                    N.stream(), tag=tag)
+                    N.stream(), tag=tag, nbytes=nbd)
         return gin
     y_prev, st_prev, pmode = prev
     T = N.call("ebsdvae_conv3x3_split_stat_tiles" if wd.pieces else "ebsdvae_conv3x3_stat_tiles",
@@ -624,10 +635,10 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
             part.data_ptr(), B, H, W, layer.cout, layer.cin)
     if wd.pieces:
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_split", *args, wd.pieces,
-                N.stream(), tag=tag + " +inbwd", pieces=wd.pieces)
+                N.stream(), tag=tag + " +inbwd", pieces=wd.pieces, nbytes=nbd)
     else:
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd", *args, N.stream(),
-                tag=tag + " +inbwd")
+                tag=tag + " +inbwd", nbytes=nbd)
     return gin, part
 
 

@@ -96,6 +96,11 @@ class VAETrainer:
         self.noise_counter = torch.zeros(1, device=dev, dtype=torch.int64)
         self.reducer = GradReducer(self.gflat, self.split, group)
         self.world = self.reducer.world
+        if self.world > 1:
+            # every rank starts from rank 0's parameters (broadcast once
+            # at init; Lightning DDP does the same when it wraps the model)
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast(self.flat, src=src, group=group)
         self._eps = None
         self.graph = None
         self._static = None

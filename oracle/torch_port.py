@@ -65,4 +65,15 @@ class CPUStep:
         out = loss(z, x_hat, mu, std, x, self.kl_lambda)
         out["loss"].backward()
         self.opt.step()
-        return float(out["loss"])
+        return float(out["loss"].detach())
+
+    @torch.no_grad()
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        """Encoder + mu head (what build_dictionary keeps, latice/index/dp_indexer.py:284-287)."""
+        a = x
+        for i, idx in enumerate(ENC_IDX):
+            a = F.conv2d(a, self.p[f"encoder.{idx}.0.weight"], self.p[f"encoder.{idx}.0.bias"], padding=1)
+            a = F.leaky_relu(F.instance_norm(a, eps=1e-5), 0.02)
+            if i % 2 == 1:
+                a = F.max_pool2d(a, 2, 2)
+        return F.linear(a.flatten(1, -1), self.p["mu.0.weight"], self.p["mu.0.bias"])

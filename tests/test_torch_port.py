@@ -34,3 +34,12 @@ def test_cpu_step_runs():
     l0 = st.step(x, torch.zeros(2, 16))
     l1 = st.step(x, torch.zeros(2, 16))
     assert np.isfinite(l0) and np.isfinite(l1)
+
+
+def test_cpu_encoder_matches_reference_mu():
+    """CPUStep.encode (the c4 cpu_baseline leg) == the reference's mu on the golden fixture."""
+    f = O.load_fixture(os.path.join(GOLDEN, "vae128_b4.npz"))
+    B, S, L, ws, xs = (int(v) for v in f["meta"])
+    st = TP.CPUStep(seeded_state_dict(ws, 32, L, S))
+    mu = st.encode(torch.from_numpy(f["x"]))
+    assert O.rel_err(mu.numpy(), f["mu"]) < 1e-5
