@@ -626,7 +626,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     int b0, h0, ch;
     coords(it, b0, h0, ch);
     sb0[sl] = b0; sh0[sl] = h0; sch[sl] = ch;
-    if constexpr (GS) gsc[sl] = ldexpf(1.f, gshift(b0));
+    // GS: the scale of the image this wave stages (NI > 1: one image per wave group)
+    if constexpr (GS) gsc[sl] = ldexpf(1.f, gshift(NI == 1 ? b0 : min(b0 + img_u, B - 1)));
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)b0 * Hs * Ws * Cin), 0,
                                                       NI == 1 ? img_bytes : img_bytes * min(NI, B - b0),
                                                       0x00020000);
@@ -724,7 +725,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const int wpx0 = fpx0 - im * tpx;
     if constexpr (NP == NP_F16) {   // undo the weight [and gradient] scale (powers of two)
       float sc = 1.f / kF16WScale;
-      if constexpr (GS) sc = ldexpf(sc, -gshift(b0 + im));
+      if constexpr (GS) sc = ldexpf(sc, -gshift(min(b0 + im, B - 1)));
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
@@ -763,9 +764,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const char* lx = lx0 + P * xslab;
     const char* lw = lw0 + P * WSLABP;
     char* lxn = lx0 + (1 - P) * xslab;
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      bf16x8 a[NPC][MF], b[NPC][NF];
+    // fragments of k-step s live in register set s & 1: the LDS reads of k-step s+1 are
+    // issued before the MFMAs of k-step s, so only k-step 0 waits on an LDS latency
+    bf16x8 fa[2][NPC][MF], fb[2][NPC][NF];
+    auto load_frags = [&](int s, bf16x8 (&a)[NPC][MF], bf16x8 (&b)[NPC][NF]) EV_LAMBDA_INLINE {
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
         const char* pa = lx + (abase[mf] + toff[s]) * XPS;
@@ -779,6 +781,20 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #pragma unroll
         for (int i = 0; i < NPC; ++i) b[i][nf] = lds_frag(pb + i * NT * 16);
       }
+    };
+#ifndef EV_PIPE_NO_FRAG_PREFETCH
+    load_frags(0, fa[0], fb[0]);
+#endif
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+#ifndef EV_PIPE_NO_FRAG_PREFETCH
+      if (s + 1 < 5) load_frags(s + 1, fa[(s + 1) & 1], fb[(s + 1) & 1]);
+#else
+      load_frags(s, fa[s & 1], fb[s & 1]);
+#endif
+      bf16x8 (&a)[NPC][MF] = fa[s & 1];
+      bf16x8 (&b)[NPC][NF] = fb[s & 1];
+#ifndef EV_PIPE_NOMFMA   // timing experiment only: one MFMA per fragment pair (wrong results)
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
@@ -792,6 +808,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
           acc[mf][nf] = mfma_piece<NP>(a[0][mf], b[1][nf], acc[mf][nf]);
           acc[mf][nf] = mfma_piece<NP>(a[0][mf], b[0][nf], acc[mf][nf]);
         }
+#else
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) acc[mf][nf] = mfma_piece<NP>(a[0][mf] + a[1][mf], b[0][nf] + b[1][nf], acc[mf][nf]);
+#endif
 #ifdef EV_PIPE_LATE_ISSUE
       if (s == 0) {   // behind the first k-step's MFMAs, so the matrix pipe covers the issue
         issue_weights(it1, lw0 + (1 - P) * WSLABP);
@@ -800,10 +822,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #endif
       // staging of it+1, spread over the k-steps (PD = 1: its loads were issued this
       // iteration, so stage after the last k-step's MFMAs are queued)
+#ifndef EV_PIPE_NOSTAGE   // timing experiment only: no staging VALU (wrong results)
 #pragma unroll
       for (int k = 0; k < KX; ++k)
         if ((PD == 2 ? (k * 5) / KX : 4) == s && item_live(k))
           stage_item(std::integral_constant<int, SL_ST>(), k, fs, lxn);
+#endif
 #ifndef EV_PIPE_NO_SCHED_FENCE
       __builtin_amdgcn_sched_barrier(0);   // one scheduling region per k-step (VGPR budget)
 #endif
@@ -956,7 +980,8 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   if (H * W < c->M) {
     // 8x8 maps (bf16x6, 128 channels): tiles of two whole images, 128 pixels, 8 waves of
     // 64 px x 32 co; pipelined kernel only
-    if (!(np == 3 && cout == 128 && H * W == 64 && use_pipe() && use_multi_image())) return false;
+    if (!((np == 3 || np == NP_F16) && cout == 128 && H * W == 64 && use_pipe() && use_multi_image()))
+      return false;
     c->M = 128;
     c->NI = 2;
     c->TH = H;
@@ -1056,7 +1081,9 @@ static void dispatch_split(const X3Cfg& c, int np, const float* src, const float
     else
       launch_x3<2, 4, 4, 2, 1, 7>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
   } else if (np == NP_F16) {
-    if (cout == 128)
+    if (cout == 128 && c.NI > 1)   // two 8x8 images per tile
+      launch_x3<NP_F16, 8, 2, 2, 1, 1, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else if (cout == 128)
       launch_x3<NP_F16, 8, 4, 2, 2, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 64)
       launch_x3<NP_F16, 8, 8, 2, 2, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);

@@ -302,8 +302,9 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     const float* __restrict__ gsrc, const float* __restrict__ w14, const float* __restrict__ y,
     const float2* __restrict__ st, const float2* __restrict__ bst, const float* __restrict__ x,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart,
-    float* __restrict__ gy, int H, int W, int T) {
+    float* __restrict__ gy, int H, int W, int T, float* __restrict__ gmax) {
   constexpr int C = 32, CG = 8, NPR = 32;
+  float amax = 0.f;   // FINAL apply: max |gy| of this thread (gmax: per-tile maxima, f16 convs)
   __shared__ double red[2][4][256];
   __shared__ float wred[4][CG][37];
   const int tile = blockIdx.x, b = blockIdx.y;
@@ -442,8 +443,10 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
         }
       }
     }
-    if (APPLY && FUSE == FUSE_FINAL)
+    if (APPLY && FUSE == FUSE_FINAL) {
       st4(gy + ((size_t)b * H * W + p) * C + c, make_float4(o[0], o[1], o[2], o[3]));
+      amax = fmaxf(fmaxf(amax, fmaxf(fabsf(o[0]), fabsf(o[1]))), fmaxf(fabsf(o[2]), fabsf(o[3])));
+    }
     }
     if (PF) {
 #pragma unroll
@@ -451,6 +454,13 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     }
   }
   const int slice = b * T + tile;
+  if (FUSE == FUSE_FINAL && APPLY && gmax) {   // block-uniform: one maximum per (image, tile)
+    __shared__ float wmax[4];
+    for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+    if (lane == 0) wmax[wave] = amax;
+    __syncthreads();
+    if (tid == 0) gmax[slice] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  }
   if (!APPLY) {   // InstanceNorm-backward plane partials (double, fixed order)
 #pragma unroll
     for (int k = 0; k < 4; ++k) { red[0][k][tid] = a1[k]; red[1][k][tid] = a2[k]; }
@@ -628,7 +638,8 @@ extern "C" int ebsdvae_in_bwd_final_reduce(const float* g1, const float* w14, co
   EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, false>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)nullptr,
-                     (const float*)nullptr, (double2*)part, wpart, bpart, (float*)nullptr, H, W, T);
+                     (const float*)nullptr, (double2*)part, wpart, bpart, (float*)nullptr, H, W, T,
+                     (float*)nullptr);
   return evh::check_launch("in_bwd_final_reduce");
 }
 
@@ -642,8 +653,25 @@ extern "C" int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, con
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)bstats,
                      (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
-                     H, W, T);
+                     H, W, T, (float*)nullptr);
   return evh::check_launch("in_bwd_final_apply");
+}
+
+extern "C" int ebsdvae_in_bwd_final_tiles(int H, int W) { return in_bwd_tiles_host(H, W); }
+
+extern "C" int ebsdvae_in_bwd_final_apply_max(const float* g1, const float* w14, const float* y,
+                                              const float* stats, const float* bstats, float* gy,
+                                              float* gmax, int B, int H, int W, int C,
+                                              ebsdvae_stream_t stream) {
+  EV_REQUIRE(g1 && w14 && y && stats && bstats && gy && gmax && C == 32,
+             "in_bwd_final_apply_max: bad args (C must be 32)");
+  const int T = in_bwd_tiles_host(H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
+                     (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)bstats,
+                     (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
+                     H, W, T, gmax);
+  return evh::check_launch("in_bwd_final_apply_max");
 }
 
 extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float* y,
@@ -657,6 +685,6 @@ extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float*
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, gnext, (const float*)nullptr, y, (const float2*)stats,
                      (const float2*)bstats, x, (double2*)nullptr, wpart, bpart, (float*)nullptr, H, W,
-                     T);
+                     T, (float*)nullptr);
   return evh::check_launch("in_bwd_first_apply_wgrad");
 }

@@ -61,6 +61,8 @@ SIGNATURES = {
     "ebsdvae_upsample2_bwd": [P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_final_reduce": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_final_apply": [P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_final_tiles": [I, I],
+    "ebsdvae_in_bwd_final_apply_max": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
@@ -88,7 +90,7 @@ _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": 
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
            "ebsdvae_wgrad_reduce_batch_work", "ebsdvae_cosine_topk_work",
-           "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
+           "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_in_bwd_final_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
            "ebsdvae_conv3x3_split_pool_ok",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices"}

@@ -315,9 +315,10 @@ def _pack_numel(layer: ConvLayer, pieces: int, dgrad: bool) -> int:
     return N.call("ebsdvae_pack_split_bytes", ci_, co_, pieces) // 4
 
 
-def pack_weight(w, layer: ConvLayer, dgrad: bool) -> PackedW:
+def pack_weight(w, layer: ConvLayer, dgrad: bool, scaled: bool = False) -> PackedW:
+    """scaled: the input-gradient operand will carry per-tile maxima (split-fp16 dgrad)."""
     ci_, co_ = (layer.cout, layer.cin) if dgrad else (layer.cin, layer.cout)
-    np_ = split_pieces(layer.H, ci_, co_, dgrad)
+    np_ = split_pieces(layer.H, ci_, co_, dgrad, scaled)
     out = _empty(_pack_numel(layer, np_, dgrad), like=w)
     if np_:
         d = (N.PackDesc * 1)(N.PackDesc(N.ptr(w), N.ptr(out), layer.cin, layer.cout, layer.kind, int(dgrad)))
@@ -338,9 +339,8 @@ class PackSet:
         descs = {}
         for i, L in enumerate(plan.enc):
             self._add(L, params[L.name + ".weight"], dgrad=i > 0, descs=descs)
-        for L in plan.dec:   # the last block's gy comes from in_backward_final (no maxima)
-            self._add(L, params[L.name + ".weight"], dgrad=True, descs=descs,
-                      scaled=L is not plan.dec[-1])
+        for L in plan.dec:   # every gy comes with per-tile maxima (in_backward[_final])
+            self._add(L, params[L.name + ".weight"], dgrad=True, descs=descs)
         self.batches = []
         for np_, lst in sorted(descs.items()):
             if len(lst) > N.MAX_PACK:
@@ -509,8 +509,15 @@ def in_backward_final(g1, w14, y, st, dw14, db14):
            part.data_ptr(), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
     bst = _in_bwd_stats(B, C, T, H * W, part, y)
     gy = torch.empty_like(y)
-    N.call("ebsdvae_in_bwd_final_apply", N.ptr(g1), N.ptr(w14), N.ptr(y), N.ptr(st), N.ptr(bst),
-           N.ptr(gy), B, H, W, C, N.stream())
+    if _FWD_PIECES.get(_PRECISION):
+        # per-tile max |gy|: the scale of the split-fp16 convs that consume gy
+        gmax = _empty(B, N.call("ebsdvae_in_bwd_final_tiles", H, W), like=y)
+        N.call("ebsdvae_in_bwd_final_apply_max", N.ptr(g1), N.ptr(w14), N.ptr(y), N.ptr(st),
+               N.ptr(bst), N.ptr(gy), N.ptr(gmax), B, H, W, C, N.stream())
+        gy.ev_gmax = gmax
+    else:
+        N.call("ebsdvae_in_bwd_final_apply", N.ptr(g1), N.ptr(w14), N.ptr(y), N.ptr(st), N.ptr(bst),
+               N.ptr(gy), B, H, W, C, N.stream())
     _reduce_slices(wpart, bpart, S_, C, 1, KIND_CONV, dw14, db14)
     return gy
 
@@ -586,7 +593,7 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
     2x2-summed, i.e. at the previous block's resolution (then in_backward takes it as P_ID)."""
     B, H, W, _ = gy.shape
     if wd is None:
-        wd = pack_weight(w, layer, dgrad=True)
+        wd = pack_weight(w, layer, dgrad=True, scaled=getattr(gy, "ev_gmax", None) is not None)
     if (sum_up and prev is not None and prev[2] == P_UP and wd.pieces
             and os.environ.get("EBSDVAE_UPSUM", "1") != "0"
             and N.call("ebsdvae_conv3x3_split_pool_ok", H, W, layer.cout, layer.cin, wd.pieces)):

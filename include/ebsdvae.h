@@ -246,6 +246,13 @@ int ebsdvae_in_bwd_final_reduce(const float* g1, const float* w14, const float* 
 int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, const float* y,
                                const float* stats, const float* bstats, float* gy, int B, int H,
                                int W, int C, ebsdvae_stream_t stream);
+/* As ebsdvae_in_bwd_final_apply, and also writes gmax[b * T + t] = max |gy| over row band t
+ * of image b, T = ebsdvae_in_bwd_final_tiles(H, W): the gradient scale of the split-fp16
+ * input- and weight-gradient convs that consume gy. */
+int ebsdvae_in_bwd_final_tiles(int H, int W);
+int ebsdvae_in_bwd_final_apply_max(const float* g1, const float* w14, const float* y,
+                                   const float* stats, const float* bstats, float* gy, float* gmax,
+                                   int B, int H, int W, int C, ebsdvae_stream_t stream);
 int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float* y, const float* stats,
                                      const float* bstats, const float* x, float* wpart,
                                      float* bpart, int B, int H, int W, int C,

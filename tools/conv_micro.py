@@ -35,6 +35,7 @@ CASES = {
     "dgrad32": ("dgrad", 128, 32, 32, P_ID),
     "dgrad64": ("dgrad", 64, 64, 64, P_ID),
     "dgrad32u": ("dgrad", 128, 32, 32, P_UP),
+    "dgrad128": ("dgrad", 32, 128, 128, P_ID),
     "wgrad32": ("wgrad", 128, 32, 32, ACT_NORM),
     "wgrad32u": ("wgrad", 128, 32, 32, ACT_NORM_UP),
     "wgrad64": ("wgrad", 64, 64, 64, ACT_NORM),
@@ -85,7 +86,14 @@ def run(name, reps, pieces, B, warm=1.0):
         T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, H, cin)
         part = torch.empty(B, T, cin, 2, dtype=torch.float64, device=dev)
 
+        gmx = gy.abs().reshape(B, 4, -1).amax(2).contiguous()   # per-tile maxima (f16)
+
         def launch():
+            if pieces == 16:
+                N.call("ebsdvae_conv3x3_dgrad_inbwd_f16", gy.data_ptr(), gmx.data_ptr(), 4, wp.data_ptr(),
+                       gin.data_ptr(), yprev.data_ptr(), stp.data_ptr(), mode, part.data_ptr(), B, H, H,
+                       cout, cin, s)
+                return
             N.call("ebsdvae_conv3x3_dgrad_inbwd_split", gy.data_ptr(), wp.data_ptr(), gin.data_ptr(),
                    yprev.data_ptr(), stp.data_ptr(), mode, part.data_ptr(), B, H, H, cout, cin, pieces, s)
     else:
@@ -97,7 +105,13 @@ def run(name, reps, pieces, B, warm=1.0):
         wpart = torch.empty(S_, 9, cout, cin, device=dev)
         bpart = torch.empty(S_, cout, device=dev)
 
+        gmx = gy.abs().reshape(B, 4, -1).amax(2).contiguous()
+
         def launch():
+            if pieces == 16:
+                N.call("ebsdvae_conv3x3_wgrad_f16", src.data_ptr(), st.data_ptr(), mode, gy.data_ptr(),
+                       gmx.data_ptr(), 4, wpart.data_ptr(), bpart.data_ptr(), B, H, H, cin, cout, s)
+                return
             N.call("ebsdvae_conv3x3_wgrad_split", src.data_ptr(), st.data_ptr(), mode, gy.data_ptr(),
                    wpart.data_ptr(), bpart.data_ptr(), B, H, H, cin, cout, pieces, s)
     for _ in range(3):
@@ -129,7 +143,7 @@ def run(name, reps, pieces, B, warm=1.0):
               f"{t[:, :, 1].mean() / tot:.3f} kloop {t[:, :, 2].mean() / tot:.3f} barrier "
               f"{t[:, :, 3].mean() / tot:.3f} epilogue {t[:, :, 4].mean() / tot:.3f}; per-wave barrier "
               + " ".join(f"{v:.2f}" for v in (t[:, :, 3].mean(0) / tot)))
-    peak = 2516.6 / {2: 3, 3: 6}[pieces]
+    peak = 2516.6 / {2: 3, 3: 6, 16: 3}[pieces]
     tf = flops / us / 1e6
     print(f"{name:12s} {kind:5s} {cin:3d}->{cout:3d} @{H:3d}  {us:8.1f} us  {tf:6.1f} TF/s  "
           f"{tf / peak:5.3f} of peak", flush=True)

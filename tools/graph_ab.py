@@ -34,3 +34,11 @@ g = timeit(tr.replay, 20)
 e2 = timeit(lambda: tr.step(x), 20)
 g2 = timeit(tr.replay, 20)
 print(f"eager {e:.3f} / {e2:.3f} ms   graph {g:.3f} / {g2:.3f} ms")
+# CPU-side enqueue time of one eager step (no synchronisation inside the measured loop)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(10):
+    tr.step(x)
+cpu = (time.perf_counter() - t0) / 10 * 1e3
+torch.cuda.synchronize()
+print(f"eager CPU enqueue {cpu:.3f} ms/step")
