@@ -73,6 +73,15 @@ EV_DEVINL void split_bf16(float x, __bf16 (&p)[NP]) {
 
 template <int NP>
 EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
+  if constexpr (NP == NP_F16) {
+    unsigned h01, l01, h23, l23;
+    split_f16x2(v.x, v.y, h01, l01);
+    split_f16x2(v.z, v.w, h23, l23);
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    out[0] = __builtin_bit_cast(bf16x4, u2{h01, h23});
+    out[1] = __builtin_bit_cast(bf16x4, u2{l01, l23});
+    return;
+  }
   const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -309,6 +318,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_split_kernel(
 // compiler from moving LDS / global accesses across it.
 // 1-KiB LDS-DMA pieces per wave and chunk of the pipelined kernel's weight slab
 constexpr int pipe_dma_per(int wslab, int nwv) { return (wslab / 1024 + nwv - 1) / nwv; }
+// halo items staged at k-step s of the pipelined kernel (item k goes to k-step k*5/KX, or all
+// to the last k-step when the prefetch distance is 1)
+constexpr int pipe_items_at(int s, int kx, int pd) {
+  int n = 0;
+  for (int k = 0; k < kx; ++k) n += ((pd == 2 ? (k * 5) / kx : 4) == s) ? 1 : 0;
+  return n;
+}
 
 template <int N>
 EV_DEVINL void pipe_barrier() {
@@ -567,28 +583,27 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   static_assert(NWV % NI == 0, "waves split evenly over the tile's images");
   const int img_w = wave / WPI;
   const int tig = tid - img_w * WPI * 64;
-  // tile-invariant item geometry: hm1 = halo row - 1 (a large negative sentinel past the halo
-  // or in a padding column), boff = the item's byte offset in its source image relative to the
-  // tile's first row (0x80000000 = always out of range), ldo = its LDS record offset
+  // tile-invariant item geometry.  Items cover the halo's interior columns only: the two
+  // zero-padding columns of every halo row are zeroed in LDS once (zero_pad_columns) and never
+  // staged.  hm1 = halo row - 1, boff = the item's byte offset in its source image relative
+  // to the tile's first row (0x80000000 = dead item, always out of range), ldo = its LDS
+  // record offset (dead items write the dummy record pixP)
+  const int NIT = (TH + 2) * W;   // staged items (pixels) per image of the tile
   int hm1[KX], boff[KX], ldo[KX];
   const int rowb = Ws * Cin * 4;   // bytes per source row
 #pragma unroll
   for (int k = 0; k < KX; ++k) {
-    const int pixl = (tig + WPI * 64 * k) >> 1;   // pixel within this image's halo
-    const int pix = img_w * pixI + (pixl < pixI ? pixl : pixP);
-    const int hh = pixl / WP, ww = pixl - hh * WP;
-    const bool in = pixl < pixI && ww >= 1 && ww <= W;
-    const int r = hh - 1, c = ww - 1;
+    const int pixl = (tig + WPI * 64 * k) >> 1;   // interior pixel within this image's halo
+    const bool in = pixl < NIT;
+    const int hh = pixl / W, c = pixl - hh * W;
+    const int r = hh - 1;
     int o;
     if (POOL) o = 2 * r * rowb + 2 * c * Cin * 4;
     else if (UPS) o = (r >> 1) * rowb + (c >> 1) * Cin * 4;
     else o = r * rowb + c * Cin * 4;
     hm1[k] = in ? r : -(1 << 28);
     boff[k] = in ? o + img_w * (Hs * Ws * Cin * 4) + q * 16 : (int)0x80000000;
-#ifdef EV_X_CONTIG   // timing experiment only: contiguous halo bytes (wrong results)
-    boff[k] = in ? (pix * 32 + q * 16) : (int)0x80000000;
-#endif
-    ldo[k] = (pixl < pixI ? pix : pixP) * XPS + q * 8;
+    ldo[k] = (in ? img_w * pixI + hh * WP + c + 1 : pixP) * XPS + q * 8;
   }
   const int img_bytes = Hs * Ws * Cin * 4;
   // item k of this wave holds at least one halo pixel (wave index made provably uniform so
@@ -596,11 +611,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int tig_u = __builtin_amdgcn_readfirstlane(tig - (tid & 63));   // the wave's first lane
   const int img_u = __builtin_amdgcn_readfirstlane(img_w);
-  auto item_live = [&](int k) EV_LAMBDA_INLINE { return (tig_u + WPI * 64 * k) < 2 * pixI; };
-
+  auto item_live = [&](int k) EV_LAMBDA_INLINE { return (tig_u + WPI * 64 * k) < 2 * NIT; };
+  // Halo rows above / below the image: their loads fall outside the buffer range and read 0,
+  // which is the right value for RAW sources of one-image tiles; the NORM transform of 0 is
+  // not 0, and with two images per tile a row outside one image is inside the other, so those
+  // stage through a row mask -- only on tiles at the top / bottom of the image (scalar flag)
+  constexpr bool MASK = NORM || NI > 1;
   float4 raw[PD][KX][NR];
   float2 st[PD][4];
-  int okm[PD];
+  int edge[PD];                    // MASK: the slot's tile touches the image top / bottom
   int sb0[PD], sh0[PD], sch[PD];   // tile image / first row / chunk of the slot's data
   float gsc[PD];                   // GS: the slot image's gradient scale
   int gs_b = -1;                   // GS: image whose shift gs_k holds
@@ -636,10 +655,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #else
     const int toff = (POOL ? 2 * h0 : (UPS ? (h0 >> 1) : h0)) * rowb + ch * XCK * 4;
 #endif
-    int m = 0;
+    if constexpr (MASK) edge[sl] = NI > 1 || h0 == 0 || h0 + TH >= H;
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
-      m |= ((unsigned)(h0 + hm1[k]) < (unsigned)H ? 1 : 0) << k;
       const int vo = boff[k] + toff;
       if (POOL) {
         raw[sl][k][0] = bload4(rs, vo);
@@ -650,7 +668,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
         raw[sl][k][0] = bload4(rs, vo);
       }
     }
-    okm[sl] = m;
     if (NORM) {
       // the chunk's 8 {mean, rstd} pairs are wave-uniform: one scalar-cache load (no TA
       // traffic), then each lane keeps its 4-channel half
@@ -663,7 +680,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     }
   };
   // transform + split item k of register slot sl into the LDS halo buffer lx
-  auto stage_item = [&](auto slot_c, int k, const float2 (&fs)[4], char* lx) EV_LAMBDA_INLINE {
+  // Branch-free so that a k-step's staging and MFMAs form one scheduling region the
+  // compiler can interleave (the edge-row mask and the activation hand-off run afterwards,
+  // in stage_post, behind uniform branches).
+  auto stage_value = [&](auto slot_c, int k, const float2 (&fs)[4]) EV_LAMBDA_INLINE {
     constexpr int sl = decltype(slot_c)::value;
     float4 v = raw[sl][k][0];
     if (POOL)
@@ -672,22 +692,44 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     if (NORM)
       v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]), normact_fs(v.z, fs[2]),
                       normact_fs(v.w, fs[3]));
-    const bool ok = (okm[sl] >> k) & 1;
-    v = make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+    return v;
+  };
+  auto stage_item = [&](auto slot_c, int k, const float2 (&fs)[4], char* lx) EV_LAMBDA_INLINE {
+    constexpr int sl = decltype(slot_c)::value;
+    float4 v = stage_value(slot_c, k, fs);
     if constexpr (GS) v = make_float4(v.x * gsc[sl], v.y * gsc[sl], v.z * gsc[sl], v.w * gsc[sl]);
-    if (act_out) {   // uniform: materialise the (pooled) activation for the wgrad
-      const int pixl = (tig + WPI * 64 * k) >> 1;
-      const int hh = pixl / WP, gw = pixl - hh * WP - 1;
-      if (ok && hh >= 1 && hh <= TH && gw >= 0 && gw < W &&
-          (NI == 1 || (pixl < pixI && sb0[sl] + img_w < B)))
-        st4(act_out + (((size_t)(sb0[sl] + img_w) * H + sh0[sl] + hh - 1) * W + gw) * Cin +
-                sch[sl] * XCK + q * 4, v);
-    }
     bf16x4 pc[NPC];
     split4<NP>(v, pc);
     char* d = lx + ldo[k];
 #pragma unroll
     for (int i = 0; i < NPC; ++i) *reinterpret_cast<bf16x4*>(d + 16 * i) = pc[i];
+  };
+  // after a halo buffer is staged (same wave, so ordered after its own writes): zero the
+  // records of halo rows outside the image (top / bottom tiles, every two-image tile), and
+  // materialise the (pooled) activation for the weight gradient when asked to (act_out)
+  auto stage_post = [&](auto slot_c, const float2 (&fs)[4], char* lx) EV_LAMBDA_INLINE {
+    constexpr int sl = decltype(slot_c)::value;
+    if constexpr (MASK) {
+      if (edge[sl]) {
+#pragma unroll
+        for (int k = 0; k < KX; ++k)
+          if ((unsigned)(sh0[sl] + hm1[k]) >= (unsigned)H) {
+            char* d = lx + ldo[k];
+#pragma unroll
+            for (int i = 0; i < NPC; ++i) *reinterpret_cast<bf16x4*>(d + 16 * i) = bf16x4{};
+          }
+      }
+    }
+    if (act_out) {
+#pragma unroll
+      for (int k = 0; k < KX; ++k) {
+        const int pixl = (tig + WPI * 64 * k) >> 1;
+        const int hh = pixl / W, gw = pixl - hh * W;
+        if (pixl < NIT && hh >= 1 && hh <= TH && (NI == 1 || sb0[sl] + img_w < B))
+          st4(act_out + (((size_t)(sb0[sl] + img_w) * H + sh0[sl] + hh - 1) * W + gw) * Cin +
+                  sch[sl] * XCK + q * 4, stage_value(slot_c, k, fs));
+      }
+    }
   };
   auto stage_fs = [&](auto slot_c, float2 (&fs)[4]) EV_LAMBDA_INLINE {
     constexpr int sl = decltype(slot_c)::value;
@@ -764,9 +806,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const char* lx = lx0 + P * xslab;
     const char* lw = lw0 + P * WSLABP;
     char* lxn = lx0 + (1 - P) * xslab;
-    // fragments of k-step s live in register set s & 1: the LDS reads of k-step s+1 are
-    // issued before the MFMAs of k-step s, so only k-step 0 waits on an LDS latency
-    bf16x8 fa[2][NPC][MF], fb[2][NPC][NF];
+    // NF == 1: fragments of k-step s live in register set s & 1, the LDS reads of k-step s+1
+    // are issued before the MFMAs of k-step s, so only k-step 0 waits on an LDS latency.
+    // NF > 1 has twice the MFMAs per k-step to cover the reads and no VGPRs to spare for a
+    // second set (it would spill): one set, read at the start of each k-step
+    constexpr bool FPF = NF == 1;
+    bf16x8 fa[FPF ? 2 : 1][NPC][MF], fb[FPF ? 2 : 1][NPC][NF];
     auto load_frags = [&](int s, bf16x8 (&a)[NPC][MF], bf16x8 (&b)[NPC][NF]) EV_LAMBDA_INLINE {
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
@@ -782,18 +827,17 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
         for (int i = 0; i < NPC; ++i) b[i][nf] = lds_frag(pb + i * NT * 16);
       }
     };
-#ifndef EV_PIPE_NO_FRAG_PREFETCH
-    load_frags(0, fa[0], fb[0]);
-#endif
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-#ifndef EV_PIPE_NO_FRAG_PREFETCH
-      if (s + 1 < 5) load_frags(s + 1, fa[(s + 1) & 1], fb[(s + 1) & 1]);
-#else
-      load_frags(s, fa[s & 1], fb[s & 1]);
-#endif
-      bf16x8 (&a)[NPC][MF] = fa[s & 1];
-      bf16x8 (&b)[NPC][NF] = fb[s & 1];
+    if constexpr (FPF) load_frags(0, fa[0], fb[0]);
+    auto kstep = [&](auto s_c) EV_LAMBDA_INLINE {
+      constexpr int s = decltype(s_c)::value;
+      constexpr int fs_ = FPF ? (s & 1) : 0;
+      if constexpr (FPF) {
+        if constexpr (s + 1 < 5) load_frags(s + 1, fa[(s + 1) & 1], fb[(s + 1) & 1]);
+      } else {
+        load_frags(s, fa[0], fb[0]);
+      }
+      bf16x8 (&a)[NPC][MF] = fa[fs_];
+      bf16x8 (&b)[NPC][NF] = fb[fs_];
 #ifndef EV_PIPE_NOMFMA   // timing experiment only: one MFMA per fragment pair (wrong results)
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
@@ -823,15 +867,40 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
       // staging of it+1, spread over the k-steps (PD = 1: its loads were issued this
       // iteration, so stage after the last k-step's MFMAs are queued)
 #ifndef EV_PIPE_NOSTAGE   // timing experiment only: no staging VALU (wrong results)
+      // every item is staged (dead ones load nothing and write the dummy record), so the
+      // region has no branch
 #pragma unroll
       for (int k = 0; k < KX; ++k)
-        if ((PD == 2 ? (k * 5) / KX : 4) == s && item_live(k))
+        if ((PD == 2 ? (k * 5) / KX : 4) == s)
           stage_item(std::integral_constant<int, SL_ST>(), k, fs, lxn);
+#endif
+#ifdef EV_PIPE_GROUPS   // experiment: measured slower for the input-gradient convs
+      // interleave: the next k-step's fragment reads, then each MFMA followed by its share of
+      // the staging VALU, so the vector work issues in the matrix pipe's shadow
+      {
+        constexpr int NMF = MF * NF * (NP == 3 ? 6 : 3);
+        constexpr int NIS = pipe_items_at(s, KX, PD);
+        constexpr int VPI = (NORM ? 12 : 0) + (POOL ? 12 : 0) + (GS ? 4 : 0) + (NPC == 2 ? 6 : 12);
+        constexpr int VPM = (NIS * VPI + NMF - 1) / NMF;
+        if constexpr (FPF && s + 1 < 5)
+          __builtin_amdgcn_sched_group_barrier(0x100, NPC * (MF + NF), 0);   // DS reads
+#pragma unroll
+        for (int i = 0; i < NMF; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                   // MFMA
+          if (VPM) __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);       // VALU
+        }
+      }
 #endif
 #ifndef EV_PIPE_NO_SCHED_FENCE
       __builtin_amdgcn_sched_barrier(0);   // one scheduling region per k-step (VGPR budget)
 #endif
-    }
+    };
+    kstep(std::integral_constant<int, 0>());
+    kstep(std::integral_constant<int, 1>());
+    kstep(std::integral_constant<int, 2>());
+    kstep(std::integral_constant<int, 3>());
+    kstep(std::integral_constant<int, 4>());
+    stage_post(std::integral_constant<int, SL_ST>(), fs, lxn);
     EV_TACC(tr_k, tb1);
     EV_T(tb2);
     if (PD == 2) {
@@ -849,6 +918,18 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   // segment (MI355X_MICROARCH.md, two waves per SIMD): raise it once
   if (wave >= NWV / 2) __builtin_amdgcn_s_setprio(1);
 #endif
+  // the zero-padding columns of both halo buffers (never staged; every chunk and tile of the
+  // block has them at the same records): 16-B granules of the NPC piece slots
+  {
+    const int nrec = 2 * NI * (TH + 2) * 2;   // buffer x image x halo row x {left, right}
+    for (int i = tid; i < nrec * NPC; i += NWV * 64) {
+      const int rec = i / NPC, pc = i - rec * NPC;
+      const int side = rec & 1, row = (rec >> 1) % (TH + 2), rest = (rec >> 1) / (TH + 2);
+      const int img = rest % NI, buf = rest / NI;
+      char* d = lx0 + buf * xslab + (img * pixI + row * WP + side * (W + 1)) * XPS + 16 * pc;
+      *reinterpret_cast<float4*>(d) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   // prologue: weights + halo of it 0 (and the halo of it 1 for PD = 2)
   zero_acc();
   issue_weights(0, lw0);
@@ -860,6 +941,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #pragma unroll
     for (int k = 0; k < KX; ++k)
       if (item_live(k)) stage_item(std::integral_constant<int, 0>(), k, fs, lx0);
+    stage_post(std::integral_constant<int, 0>(), fs, lx0);
   }
   __syncthreads();
   // nch = Cin / 8 is even for every supported layer (plan_split), so it & 1 == ch & 1
@@ -993,8 +1075,12 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   const int pixI = (c->TH + 2) * (W + 2);
   const int pix = c->NI * pixI;
   const int tpg = (c->nwv / c->NI) * 64;   // threads staging one image's halo
-  c->KX = (pixI * 2 + tpg - 1) / tpg;
-  const int kxmax = np == 2 ? (cout == 128 ? 2 : (cout == 64 ? 5 : 7)) : (cout == 128 ? 2 : (cout == 64 ? 4 : 5));
+  // pipelined kernel: interior columns only; the non-persistent kernel stages whole halo rows
+  c->KX = use_pipe() ? ((c->TH + 2) * W * 2 + tpg - 1) / tpg : (pixI * 2 + tpg - 1) / tpg;
+  // the item count each dispatch_split instantiation is compiled for
+  const int kxmax = np == 2 ? (cout == 128 ? 2 : (cout == 64 ? 5 : 7))
+                            : (np == NP_F16 ? (cout == 128 ? 2 : (cout == 64 ? 3 : 4))
+                                            : (cout == 128 ? 2 : (cout == 64 ? 4 : 5)));
   if (c->KX > kxmax) return false;
   const int wslab = XTAPS * npc(np) * cout * 16;
   c->lds = 2 * (size_t)wslab + 2 * (size_t)(pix + 1) * XPS;
@@ -1086,9 +1172,11 @@ static void dispatch_split(const X3Cfg& c, int np, const float* src, const float
     else if (cout == 128)
       launch_x3<NP_F16, 8, 4, 2, 2, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 64)
-      launch_x3<NP_F16, 8, 8, 2, 2, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
-    else
-      launch_x3<NP_F16, 8, 8, 2, 1, 5>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+      launch_x3<NP_F16, 8, 8, 2, 2, 3>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else if (c.KX <= 3)
+      launch_x3<NP_F16, 8, 8, 2, 1, 3>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else   // 256-wide maps: two-row tiles, four items per thread
+      launch_x3<NP_F16, 8, 8, 2, 1, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
   } else {
     if (cout == 128 && c.NI > 1)   // two 8x8 images per tile: 2 x 4 waves of 64 px x 32 co
       launch_x3<3, 8, 2, 2, 1, 1, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);

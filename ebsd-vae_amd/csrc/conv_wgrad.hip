@@ -352,8 +352,17 @@ EV_DEVINL bf16x8w tr_frag(const char* r0, const char* r1) {
 
 template <int NP>
 EV_DEVINL void store_pieces(char* base, size_t piece_stride, float4 v) {
-  const float e[4] = {v.x, v.y, v.z, v.w};
   typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+  if constexpr (NP == NP_F16) {   // fp16 bit patterns in the 16-bit piece slots
+    unsigned h01, l01, h23, l23;
+    split_f16x2(v.x, v.y, h01, l01);
+    split_f16x2(v.z, v.w, h23, l23);
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<u2*>(base) = u2{h01, h23};
+    *reinterpret_cast<u2*>(base + piece_stride) = u2{l01, l23};
+    return;
+  }
+  const float e[4] = {v.x, v.y, v.z, v.w};
   constexpr int NPC = npc(NP);
   bf4 pc[NPC];
 #pragma unroll
