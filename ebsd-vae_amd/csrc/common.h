@@ -109,10 +109,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ---- split-fp16 piece format ("f16x3", include/ebsdvae.h EBSDVAE_PIECES_F16): two fp16
 // pieces x0 = f16(x), x1 = f16(x - x0) per operand, products a0b0 + a0b1 + a1b0 on the fp16
-// MFMA.  Weights are packed as w * kF16WScale; gradient operands are scaled by a power of
-// two from their maximum (f16_shift) so that both sit inside fp16's range.
+// MFMA.  Weights are packed as w * 2^k with one power of two per layer from its max |w|
+// (f16_wshift, stored in the pack's trailer); gradient operands are scaled by a power of two
+// from their maximum (f16_shift) so that both sit inside fp16's range.
 constexpr int NP_F16 = 16;   // == EBSDVAE_PIECES_F16
-constexpr float kF16WScale = 256.f;
+constexpr int kF16PackTrailer = 16;   // bytes after the split-fp16 pack: int32 weight shift k
 constexpr int npc(int np) { return np == NP_F16 ? 2 : np; }   // pieces per operand
 
 // Two floats -> their split-fp16 pieces, packed: hi = (f16(a), f16(b)) round-to-nearest

@@ -61,15 +61,16 @@ EV_DEVINL void split_bf16(float x, __bf16 (&p)[NP]) {
   }
 }
 
-// Piece format NP_F16 ("f16x3", forward convs only): two fp16 pieces
+// Piece format NP_F16 ("f16x3"): two fp16 pieces
 //     x0 = f16(x), x1 = f16(x - x0)      (11 significand bits each, |x - x0 - x1| <= 2^-23 |x|
 //                                          for normal x1, 2^-25 absolute below it)
 // and the three products a0b0 + a0b1 + a1b0 on v_mfma_f32_32x32x16_f16 (the dropped a1b1 is
 // <= 2^-24 relative): ~2^-22.5 per product, at the bf16x3 rate.  fp16's range is narrow, so
-// the weights are packed as w * kF16WScale (2^8: small weights keep x1 in the normal range;
-// |w| < 255 stays finite) and the epilogue multiplies the accumulators by the exact inverse.
-// The forward operands are normalised activations (IN + LeakyReLU, |x| <= sqrt(H*W)), which
-// fp16 holds; gradients span far smaller magnitudes, so dgrad / wgrad stay on bf16x6.
+// the weights of each layer are packed as w * 2^k, k from the layer's max |w| (max |w| 2^k in
+// [2^11, 2^12): pack_wshift_kernel, stored in the pack's trailer) and the epilogue multiplies
+// the accumulators by the exact 2^-k.  Forward operands are normalised activations
+// (IN + LeakyReLU, |x| <= sqrt(H*W) by construction), which fp16 holds as they are; the
+// gradient operand of input-gradient launches is scaled per image from its maxima (GS).
 
 template <int NP>
 EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
@@ -740,6 +741,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   // pieces of the last chunk fall outside the descriptor's range), so every iteration issues
   // the same, compile-time number of vector-memory ops and the compiler's waits stay exact
   const auto rwp = __builtin_amdgcn_make_buffer_rsrc((void*)wp, 0, nch * WSLAB, 0x00020000);
+  // NP_F16: the layer's weight shift k (weights packed as w * 2^k), in the pack's trailer
+  const int wshift = NP == NP_F16 ? *reinterpret_cast<const int*>(wp + (size_t)nch * WSLAB) : 0;
   auto issue_weights = [&](int it, char* lw) EV_LAMBDA_INLINE {
     const int ch = it - (it / nch) * nch;
 #pragma unroll
@@ -766,7 +769,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const int im = NI == 1 ? 0 : (wm * MW) / tpx;   // the wave's pixels lie in one image
     const int wpx0 = fpx0 - im * tpx;
     if constexpr (NP == NP_F16) {   // undo the weight [and gradient] scale (powers of two)
-      float sc = 1.f / kF16WScale;
+      float sc = ldexpf(1.f, -wshift);
       if constexpr (GS) sc = ldexpf(sc, -gshift(min(b0 + im, B - 1)));
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
@@ -966,6 +969,26 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #endif
 }
 
+// NP_F16 packs: the layer's weight shift k = f16_shift_of(max |w|) into the pack's trailer
+// (one block per layer; runs before pack_split_kernel on the same stream)
+__global__ __launch_bounds__(256) void pack_wshift_kernel(const PackBatch pb) {
+  const ebsdvae_pack_desc& q = pb.d[blockIdx.x];
+  const int n = q.cin * q.cout * 9;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(q.src[i]));
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int ci_ = q.for_dgrad ? q.cout : q.cin, co_ = q.for_dgrad ? q.cin : q.cout;
+    const size_t body = (size_t)(ci_ / XCK) * XTAPS * npc(NP_F16) * co_ * XCK * 2;
+    const float mx = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    *reinterpret_cast<int4*>(reinterpret_cast<char*>(q.dst) + body) =
+        make_int4(mx > 0.f ? f16_shift_of(mx) : 0, 0, 0, 0);   // the whole 16-byte trailer
+  }
+}
+
 // split weight pack: [chunk][tap 0..9][piece][co'][8 ci'] bf16 of the conv-equivalent
 // weight (tap 9 = 0); (ci', co') = (cin, cout) of the layer, swapped for the input gradient.
 __global__ void pack_split_kernel(const PackBatch pb, int np) {
@@ -993,7 +1016,8 @@ __global__ void pack_split_kernel(const PackBatch pb, int np) {
     }
     const size_t base = ((size_t)(chunk * XTAPS + t) * npc(np)) * co_ * XCK + (size_t)o * XCK + c8;
     if (np == NP_F16) {   // two fp16 pieces of the scaled weight (conv3x3_pipe_kernel undoes it)
-      const float ws = w * kF16WScale;
+      const int k = *reinterpret_cast<const int*>(d + (size_t)n * npc(np));   // trailer
+      const float ws = ldexpf(w, k);
       const _Float16 h0 = (_Float16)ws;
       const _Float16 h1 = (_Float16)(ws - (float)h0);
       d[base] = __builtin_bit_cast(__bf16, h0);
@@ -1211,7 +1235,8 @@ extern "C" int ebsdvae_conv3x3_split_stat_tiles(int H, int W, int cout) {
 }
 
 extern "C" size_t ebsdvae_pack_split_bytes(int cin, int cout, int pieces) {
-  return (size_t)(cin / XCK) * XTAPS * npc(pieces) * cout * XCK * 2;
+  return (size_t)(cin / XCK) * XTAPS * npc(pieces) * cout * XCK * 2 +
+         (pieces == NP_F16 ? kF16PackTrailer : 0);
 }
 
 extern "C" int ebsdvae_pack_conv_weights_split(const ebsdvae_pack_desc* descs, int n, int pieces,
@@ -1232,6 +1257,8 @@ extern "C" int ebsdvae_pack_conv_weights_split(const ebsdvae_pack_desc* descs, i
   }
   int bx = (maxn + 255) / 256;
   if (bx > 64) bx = 64;
+  if (pieces == NP_F16)
+    hipLaunchKernelGGL(pack_wshift_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, pb);
   hipLaunchKernelGGL(pack_split_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, pb, pieces);
   return evh::check_launch("pack_conv_weights_split");
 }

@@ -103,9 +103,10 @@ int ebsdvae_conv3x3_cout1_dgrad(const float* g, const float* w, float* gin, int 
  * v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
  *   pieces = 2 ("bf16x3", 3 MFMAs, ~2^-16.5 relative error per product);
  *   pieces = 3 ("bf16x6", 6 MFMAs, ~2^-25: fp32 grade);
- *   pieces = EBSDVAE_PIECES_F16 ("f16x3", forward only: two fp16 pieces x0 = f16(x),
- *     x1 = f16(x - x0) on v_mfma_f32_32x32x16_f16, 3 MFMAs, ~2^-22.5 per product; the pack
- *     holds w * 256 so small weights keep full precision, |w| < 255).
+ *   pieces = EBSDVAE_PIECES_F16 ("f16x3": two fp16 pieces x0 = f16(x), x1 = f16(x - x0) on
+ *     v_mfma_f32_32x32x16_f16, 3 MFMAs, ~2^-22.5 per product; the pack holds w * 2^k with one
+ *     power of two per layer, max |w| 2^k in [2^11, 2^12), k in a 16-byte trailer that
+ *     ebsdvae_pack_split_bytes includes, so any weight magnitude keeps fp16's full precision).
  * Weights use the split pack ([cin'/8][tap 0..9][piece][cout'][8] bf16,
  * ebsdvae_pack_split_bytes bytes).  Shapes: ebsdvae_conv3x3_split_supported; InstanceNorm
  * partials use ebsdvae_conv3x3_split_stat_tiles tiles per image.  pmode = -1 in

@@ -445,12 +445,14 @@ SPLIT_TOL = {"bf16x3": 1e-4, "bf16x6": 2e-5, "f16x3": 2e-5}
 FWD_PIECES = {"bf16x3": 2, "bf16x6": 3, "f16x3": E.PIECES_F16}
 
 
-@pytest.mark.parametrize("wscale", [0.1, 1e-3])
+@pytest.mark.parametrize("wscale", [0.1, 1e-3, 1e-5, 100.0])
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16x6", "f16x3"])
 @pytest.mark.parametrize("cin,cout,H,mode", [c for c in FWD_CASES if c[0] > 1 and c[2] >= 8])
 def test_conv3x3_fwd_split_bf16(cuda, cin, cout, H, mode, prec, wscale):
     """Split forward == float64 oracle (bf16x3 within 1e-4, bf16x6 and f16x3 at 2e-5).
-    wscale 1e-3: small weights, whose fp16 pieces rely on the pack's x256 scale."""
+    wscale 1e-3 / 1e-5 / 100: weights far from 1, which fp16 pieces hold only through the
+    pack's per-layer power-of-two scale (1e-5 unscaled would be subnormal in fp16, 100 x 256
+    would overflow the old fixed x256 scale)."""
     if wscale != 0.1 and prec != "f16x3":
         pytest.skip("weight-scale sweep targets the fp16 pieces")
     if not N.call("ebsdvae_conv3x3_split_supported", H, H, cin, cout, FWD_PIECES[prec]):
@@ -541,9 +543,10 @@ def _pack_f16_dgrad(w_d, layer):
     return E.PackedW(out, E.PIECES_F16)
 
 
+@pytest.mark.parametrize("wscale", [0.1, 1e-5, 100.0])
 @pytest.mark.parametrize("gscale", [1.0, 1e-7])
 @pytest.mark.parametrize("cin,cout,H,pmode", [c for c in FUSED_CASES if c[2] >= 8])
-def test_dgrad_fused_split_f16(cuda, cin, cout, H, pmode, gscale):
+def test_dgrad_fused_split_f16(cuda, cin, cout, H, pmode, gscale, wscale):
     """Split-fp16 input gradient (f16x3) == float64 oracle at 2e-5, with the gradient operand
     scaled per image from its maximum: images 1e3 apart in magnitude, and tiny gradients
     (1e-7: far below fp16's normal range unscaled).  Also pins the per-tile maxima that the
@@ -558,7 +561,7 @@ def test_dgrad_fused_split_f16(cuda, cin, cout, H, pmode, gscale):
     st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
     gy = rng.standard_normal((B, H, H, cout)) * gscale
     gy[1] *= 1e3
-    wsrc = rng.standard_normal((cout, cin, 3, 3)) * 0.1
+    wsrc = rng.standard_normal((cout, cin, 3, 3)) * wscale
     layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, E.ACT_RAW, 0)
     with E.precision("f16x3"):
         y_d, st_d, w_d = dev(y), dev(st), dev(wsrc)
@@ -685,20 +688,28 @@ WG_F16_CASES = [  # (cin, cout, H, source mode, kind): NORM, NORM_UP and pooled-
 ]
 
 
+@pytest.mark.parametrize("spike", [False, True])
 @pytest.mark.parametrize("spread", [1.0, 1e3])
 @pytest.mark.parametrize("gscale", [1.0, 1e-7])
 @pytest.mark.parametrize("cin,cout,H,mode,kind", WG_F16_CASES)
-def test_conv_wgrad_f16(cuda, cin, cout, H, mode, kind, gscale, spread):
+def test_conv_wgrad_f16(cuda, cin, cout, H, mode, kind, gscale, spread, spike):
     """Split-fp16 weight gradient (ebsdvae_conv3x3_wgrad_f16, the f16x3 default) == float64
     oracle at 2e-5 norm-wise.  The gradient operand is scaled per slice by a power of two
     from the per-tile maxima (gmax); gscale 1e-7 puts the unscaled gradient far below fp16's
     normal range, and spread 1e3 makes the images of one slice 1e3 apart in magnitude
-    (one scale per slice from the largest)."""
+    (one scale per slice from the largest).  The activation operand is not scaled: it is a
+    normalised activation, |xhat| <= sqrt(H*W - 1) by construction; spike puts one value per
+    plane at that bound (all others near 0) to cover the widest range it can take."""
     if not N.call("ebsdvae_conv3x3_wgrad_split_slices", 2, H, H, cin, cout, E.PIECES_F16) > 0:
         pytest.skip("shape not covered by the f16 weight gradient")
     rng = np.random.default_rng(71 + cin + cout + H + mode)
     B = 3 if H <= 64 else 2
     s, mean, rstd, st = make_src(rng, B, H, cin, mode)
+    if spike:
+        s[:, 1, 2, :] = 1e6
+        mean = s.mean(axis=(1, 2), keepdims=True)
+        rstd = 1.0 / np.sqrt(s.var(axis=(1, 2), keepdims=True) + 1e-5)
+        st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
     gy = rng.standard_normal((B, H, H, cout)) * gscale
     gy[0] /= spread
     wshape = (cout, cin, 3, 3) if kind == 0 else (cin, cout, 3, 3)
@@ -724,3 +735,29 @@ def test_conv_wgrad_f16(cuda, cin, cout, H, mode, kind, gscale, spread):
         rw = rw.transpose(1, 0, 2, 3)[:, :, ::-1, ::-1]
     assert O.rel_err(host(dw), rw) < SPLIT_TOL["f16x3"]
     assert O.rel_err(host(db), rb) < 5e-5
+
+
+def test_f16_weight_pack_trailer_and_batch(cuda):
+    """Split-fp16 packs: the batched PackSet launch == per-layer packs bit for bit (pieces and
+    the per-layer weight-shift trailer), and the trailer holds k with max|w| 2^k in
+    [2^11, 2^12) for weights of very different magnitudes."""
+    plan = E.build_plan(32, 16, 128)
+    rng = np.random.default_rng(19)
+    params = {}
+    for i, L in enumerate(plan.enc + plan.dec):
+        shape = (L.cout, L.cin, 3, 3) if L.kind == E.KIND_CONV else (L.cin, L.cout, 3, 3)
+        params[L.name + ".weight"] = dev(rng.standard_normal(shape) * 10.0 ** (i % 7 - 4))
+    with E.precision("f16x3"):
+        packs = E.PackSet(plan, params).refresh()
+        for L in plan.enc[1:] + plan.dec:
+            w = params[L.name + ".weight"]
+            pf, pd = packs[L.name]
+            single = E.pack_weight(w, L, dgrad=False)
+            assert pf.pieces == single.pieces and torch.equal(pf.t, single.t), L.name
+            if pf.pieces == E.PIECES_F16:
+                k = int(pf.t[-4:].view(torch.int32)[0])
+                m = float(w.abs().max())
+                assert 2.0 ** 11 <= m * 2.0 ** k < 2.0 ** 12, (L.name, m, k)
+            if pd is not None:
+                single = E.pack_weight(w, L, dgrad=True, scaled=True)
+                assert pd.pieces == single.pieces and torch.equal(pd.t, single.t), L.name
