@@ -456,6 +456,32 @@ def _in_bwd_stats(B, C, T, HW, part, like):
     return bst
 
 
+# ----------------------------------------------------------------------------- side stream
+# Weight gradients are off the backward's critical path (in_backward -> input gradient -> ...):
+# they run on a second HIP stream, so they overlap the memory-bound InstanceNorm-backward passes
+# and the other kernels' tails.  The side stream waits for the main stream before each weight
+# gradient (its inputs are ready), the slice reductions run on the main stream after joining
+# it; record_stream keeps the caching allocator from recycling a buffer one stream still uses.
+# EBSDVAE_WGRAD_STREAM=0 keeps everything on the current stream.
+_WG_STREAM = os.environ.get("EBSDVAE_WGRAD_STREAM", "1") != "0"
+_SIDE = {}
+
+
+def _side_stream(device):
+    if not _WG_STREAM or torch.cuda.is_current_stream_capturing():
+        return None
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
+def _join_side(device):
+    side = _SIDE.get(device.index if device.index is not None else torch.cuda.current_device())
+    if side is not None:
+        torch.cuda.current_stream(device).wait_stream(side)
+
+
 # Weight-gradient slice reductions queued inside `batched_wgrad_reduce()` run as ONE batched
 # pair of launches when the block exits (ebsdvae_wgrad_reduce_batch) instead of two launches
 # per layer; outside such a block they run immediately.  Results are bit-identical.
@@ -475,6 +501,8 @@ def batched_wgrad_reduce():
 
 
 def _flush_reduces(q):
+    if q:
+        _join_side(q[0][0].device)
     for i in range(0, len(q), N.MAX_WGRAD_BATCH):
         chunk = q[i:i + N.MAX_WGRAD_BATCH]
         descs = (N.WgradReduceDesc * len(chunk))(*[
@@ -487,9 +515,13 @@ def _flush_reduces(q):
 
 
 def _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db):
+    main = torch.cuda.current_stream(wpart.device)
+    for t in (wpart, bpart):   # partials written on the side stream, read on this one
+        t.record_stream(main)
     if _RQ is not None:
         _RQ.append((wpart, bpart, S_, cin, cout, kind, dw, db))
         return
+    _join_side(wpart.device)
     nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
     work = torch.empty(nbytes // 8, dtype=torch.float64, device=wpart.device)
     N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db), cin, cout,
@@ -544,7 +576,24 @@ def in_backward_first(gnext, y, st, x, dw0, db0, part=None):
 
 def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized=None):
     """normalized: src is a normalised activation (default: the NORM modes); the split-fp16
-    weight gradient (f16x3, gy with per-tile maxima) scales only gy, so it needs one."""
+    weight gradient (f16x3, gy with per-tile maxima) scales only gy, so it needs one.
+    Runs on the side stream (see _side_stream); dw/db are written by the slice reduction on
+    the caller's stream."""
+    side = _side_stream(gy.device)
+    if side is None:
+        return _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized)
+    side.wait_stream(torch.cuda.current_stream(gy.device))
+    for t in (src, src_stats, gy, getattr(gy, "ev_gmax", None)):
+        if t is not None:
+            t.record_stream(side)
+    with torch.cuda.stream(side):
+        wpart, bpart, S_ = _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db,
+                                       normalized, reduce=False)
+    _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
+
+
+def _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized=None,
+                reduce=True):
     B, H, W, _ = gy.shape if gy.dim() == 4 else (*gy.shape, 1)
     if normalized is None:
         normalized = src_mode in (ACT_NORM, ACT_NORM_UP)
@@ -561,6 +610,8 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
                     N.ptr(gmax), gmax.shape[1], N.ptr(wpart), N.ptr(bpart), B, H, W, cin, cout,
                     N.stream(), tag=f"wgrad {cin:3d}->{cout:3d} @{H:3d} m{src_mode} f16",
                     pieces=PIECES_F16, nbytes=nbw)
+            if not reduce:
+                return wpart, bpart, S_
             _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
             return
     np_ = _PIECES[_PRECISION]
@@ -582,6 +633,8 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
     else:
         _launch("conv3x3_wgrad", conv_flops(B, H, W, cin, cout), N.call, "ebsdvae_conv3x3_wgrad",
                 *args, s, tag=tag, nbytes=nbw)
+    if not reduce:
+        return wpart, bpart, S_
     _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
 
 
