@@ -919,7 +919,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #ifdef EV_PIPE_PRIO
   // the younger half of the workgroup loses VALU arbitration to the older half on every
   // segment (MI355X_MICROARCH.md, two waves per SIMD): raise it once
-  if (wave >= NWV / 2) __builtin_amdgcn_s_setprio(1);
+  if (wave_u >= NWV / 2) __builtin_amdgcn_s_setprio(1);   // scalar branch: this wave only
 #endif
   // the zero-padding columns of both halo buffers (never staged; every chunk and tile of the
   // block has them at the same records): 16-B granules of the NPC piece slots

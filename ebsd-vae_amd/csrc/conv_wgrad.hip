@@ -17,6 +17,8 @@
 // activation halo [(TH+2)(TW+2)][32] with stride 48 (same reason).  The activation is
 // recomputed from the producer's saved pre-norm output (InstanceNorm + LeakyReLU
 // [+ pool/upsample]) while staging, exactly as in the forward.
+#include <utility>
+
 #include "common.h"
 #include "../../include/ebsdvae.h"
 
@@ -85,6 +87,36 @@ static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g, int pt = 
   g->tps = tps;
   g->slices = (g->tiles + tps - 1) / tps;
   return true;
+}
+
+// the pipelined two-piece kernel (wgrad_pipe_kernel) on 8x8 tiles; EBSDVAE_WG_PIPE=0 selects
+// wgrad_split_kernel instead (A/B timing)
+static bool wg_pipe() {
+  static const bool v = [] {
+    const char* e = getenv("EBSDVAE_WG_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
+  if (H % 8 || W % 8 || cin % 32 || !(cout == 32 || cout % 64 == 0)) return false;
+  g->TW = 8; g->TH = 8; g->NI = 1;
+  g->ntx = W / 8; g->nty = H / 8;
+  g->lTW = 3; g->ltpx = 6;
+  g->tiles = (int)((long)B * g->ntx * g->nty);
+  const int co_t = cout == 32 ? 1 : cout / 64;
+  const int want = wg_block_target(64) / (co_t * (cin / 32));
+  int tps = 4;
+  while ((g->tiles + tps - 1) / tps > (want > 1 ? want : 1)) tps *= 2;
+  g->tps = tps;
+  g->slices = (g->tiles + tps - 1) / tps;
+  return true;
+}
+
+// 1-D grid of wgrad_pipe_kernel: 8 x ceil(slices / 8) x (co tiles x ci tiles) blocks
+static dim3 wg_pipe_grid(const WgGeom& g, int cin, int cout) {
+  const int nm = (cout == 32 ? 1 : cout / 64) * (cin / 32);
+  return dim3(8 * ((g.slices + 7) / 8) * nm);
 }
 
 EV_DEVINL void tile_origin(int t, const WgGeom& g, int& b0, int& y0, int& x0) {
@@ -397,6 +429,67 @@ EV_DEVINL f32x4 mfma16_piece(bf16x8w a, bf16x8w b, f32x4 c) {
 
 constexpr int WGS_ASB = 96;   // activation image row stride (32 ch x 2 B + 32 B)
 
+// End of a split weight-gradient block (both kernels below): fold the second K half into
+// the first through LDS (KSPLIT 2), store the slice's partial dW tile [slice][tap][co][ci]
+// (16x16 C/D: col = ci = lane & 15, row = co) with the gradient scale undone, and the bias
+// partial from the per-thread gy sums (ci tile 0 only).  LDS is free on entry.
+template <int NWCO, int KSPLIT, bool F16>
+EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[2][9], const double (&bs)[4], char* wsm,
+                                  float* __restrict__ wpart, float* __restrict__ bpart, int slice,
+                                  int co0, int ci0, int Cin, int Cout, float gsc, bool do_bias) {
+  constexpr int CO_T = NWCO * 32;
+  constexpr int QG = CO_T / 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
+  if (KSPLIT == 2) {
+    float* xs = reinterpret_cast<float*>(wsm) + (size_t)(wave - 2 * NWCO) * 72 * 64;
+    if (wk == 1) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xs[((f * 9 + tap) * 4 + r) * 64 + lane] = acc[f][tap][r];
+    }
+    __syncthreads();
+    if (wk == 0) {
+      xs = reinterpret_cast<float*>(wsm) + (size_t)wave * 72 * 64;
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[f][tap][r] += xs[((f * 9 + tap) * 4 + r) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  const int ci = ci0 + wci * 16 + (lane & 15);
+  if (wk == 0) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wco * 32 + f * 16 + (lane >> 4) * 4 + r;
+          wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] =
+              F16 ? acc[f][tap][r] * (1.f / gsc) : acc[f][tap][r];
+        }
+  }
+  if (do_bias) {
+    double* xb = reinterpret_cast<double*>(wsm);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xb[i * 256 + tid] = bs[i];
+    __syncthreads();
+    if (tid < CO_T) {
+      const int qq = tid >> 2, i = tid & 3;
+      double sum = 0.0;
+      for (int m = qq; m < 256; m += QG) sum += xb[i * 256 + m];
+      bpart[(size_t)slice * Cout + co0 + tid] = (float)sum;
+    }
+  }
+}
+
 template <int NP, int NWCO, int KSPLIT, int MODE, int TW, int PT>
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats,
@@ -559,10 +652,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
         hp0 = (im0 * T::HP + rm0 / TW) * T::WP + rm0 % TW;
         hp1 = (im1 * T::HP + rm1 / TW) * T::WP + rm1 % TW;
       }
+      bf16x8w b[NPC];
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int toff = (tap / 3) * T::WP + tap % 3;
-        bf16x8w b[NPC];
+#ifdef EV_WG_ONEB   // timing experiment only: one activation fragment per k-step (wrong results)
+        if (tap == 0)
+#endif
 #pragma unroll
         for (int i = 0; i < NPC; ++i)
           b[i] = tr_frag(aimg + i * ACT_PIECE + (hp0 + toff) * WGS_ASB + bcol,
@@ -591,54 +687,243 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(
     }
   }
   __syncthreads();
-  if (KSPLIT == 2) {   // fold the second K half into the first through LDS
-    float* xs = reinterpret_cast<float*>(wsm) + (size_t)(wave - 2 * NWCO) * 72 * 64;
-    if (wk == 1) {
+  wgrad_split_finish<NWCO, KSPLIT, F16>(acc, bs, wsm, wpart, bpart, slice, co0, ci0, Cin, Cout, gsc,
+                                        do_bias);
+}
+
+// f(integral_constant<int, 0>()), ..., f(integral_constant<int, N-1>()): compile-time indices
+// for register arrays and slot tests inside fully unrolled loops
+template <class F, int... I>
+EV_DEVINL void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>()), ...);
+}
+template <int N, class F>
+EV_DEVINL void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>());
+}
+
+// ------------------------------------------------------------------ pipelined split-fp16
+// wgrad_split_kernel's operand images, transposed reads and MFMA sequence on 8x8 pixel tiles
+// (100 halo pixels per 64, the fewest staged of the 64-pixel shapes), software-pipelined
+// over the slice's tiles with two LDS image sets: while the k-steps of tile t read one set,
+// tile t+1 is transformed, split and written into the other item by item BETWEEN the taps,
+// and each item's register is refilled with tile t+2's load as soon as it has been staged
+// (a whole tile of MFMA work covers every load).  One barrier per tile.  The serial kernel
+// spends most of its time there: without its staging it runs 2.3-2.7x faster, without its
+// loads 1.3x (tools/micro_variants.sh, EV_WG_NOSTORE / EV_WG_NOLOAD).
+template <int NP, int NWCO, int KSPLIT, int MODE>
+__global__ __launch_bounds__(256, 2) void wgrad_pipe_kernel(
+    const float* __restrict__ src, const float2* __restrict__ sstats,
+    const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
+    int H, int W, int Cin, int Cout, WgGeom g, const float* __restrict__ gmax, int gmT) {
+  constexpr int TW = 8, PT = 64;
+  using T = WgTileP<TW, PT>;               // one image, 8x8 pixels, 10x10 halo
+  constexpr int NPC = npc(NP);
+  constexpr bool F16 = NP == NP_F16;
+  constexpr int CO_T = NWCO * 32;
+  constexpr int GSB = CO_T * 2 + 32;       // gy image row stride (bytes)
+  constexpr int QG = CO_T / 4;
+  constexpr int KG = PT * CO_T / 4 / 256;  // gy float4 items per thread per tile
+  constexpr int KH = (T::HALO * 8 + 255) / 256;
+  constexpr int NIT = KG + KH;
+  constexpr int KSTEPS = PT / 32;
+  constexpr int NSLOT = (KSTEPS / KSPLIT) * 9;   // (k-step, tap) slots per wave and tile
+  constexpr int GY_PIECE = PT * GSB;
+  constexpr int ACT_PIECE = T::HALO * WGS_ASB;
+  constexpr int BUF = NPC * (GY_PIECE + ACT_PIECE);
+  constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_UP);
+  constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
+  static_assert(T::NI == 1 && T::HP == 10 && T::WP == 10, "8x8 tiles");
+  static_assert(NWCO * 2 * KSPLIT == 4, "4 waves per block");
+  static_assert(KSTEPS % KSPLIT == 0 && NIT <= NSLOT, "item slots");
+  static_assert(MODE != ACT_NORM_POOL, "pool-fed layers use the materialised activation");
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
+  // XCD-aware block order (1-D grid, wg_pipe_grid): blocks L and L + 8 share an XCD, so the
+  // nm = (co tiles) x (ci tiles) blocks of one slice take consecutive L / 8 on ONE XCD and
+  // read the slice's gy and activation rows while they are in that XCD's L2
+  const int nco = Cout / CO_T, nm = nco * (Cin / 32);
+  const int xcd = blockIdx.x & 7, wq = blockIdx.x >> 3, m = wq % nm;
+  const int slice = (wq / nm) * 8 + xcd;
+  if (slice >= g.slices) return;   // grid padding (whole block, before any barrier)
+  const int co0 = (m % nco) * CO_T, ci0 = (m / nco) * 32;
+  const int Hs = UPS ? H / 2 : H, Ws = UPS ? W / 2 : W;
+  const int qh = tid & 7, qg = tid % QG;
+
+  f32x4 acc[2][9];
 #pragma unroll
-      for (int f = 0; f < 2; ++f)
+  for (int f = 0; f < 2; ++f)
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap)
+    for (int t = 0; t < 9; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double bs[4] = {0.0, 0.0, 0.0, 0.0};
+
+  const int per_img = g.ntx * g.nty;
+  const int t_beg = slice * g.tps;
+  const int t_end = min(t_beg + g.tps, g.tiles);
+  int gshift = 0;   // F16: the slice's gy scale 2^k (see wgrad_split_kernel)
+  if constexpr (F16)
+    if (t_beg < t_end) gshift = f16_gshift(gmax, gmT, t_beg / per_img, (t_end - 1) / per_img);
+  const float gsc = ldexpf(1.f, gshift);
+
+  // tile-invariant item geometry: gy item k = pixel (gr, gc) of the tile, channels qg*4..;
+  // halo item k = halo pixel hp (row hh, column ww), channels qh*4.. of the ci tile
+  int gyo[KG], glo[KG];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) xs[((f * 9 + tap) * 4 + r) * 64 + lane] = acc[f][tap][r];
-    }
-    __syncthreads();
-    if (wk == 0) {
-      xs = reinterpret_cast<float*>(wsm) + (size_t)wave * 72 * 64;
-#pragma unroll
-      for (int f = 0; f < 2; ++f)
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[f][tap][r] += xs[((f * 9 + tap) * 4 + r) * 64 + lane];
-    }
-    __syncthreads();
+  for (int k = 0; k < KG; ++k) {
+    const int px = (tid + 256 * k) / QG, r = px / TW, c = px % TW;
+    gyo[k] = (r * W + c) * Cout + co0 + qg * 4;
+    glo[k] = px * GSB + qg * 8;
   }
-  // partial layout [slice][tap][co][ci]; 16x16 C/D: col = ci (lane & 15), row = co
-  const int ci = ci0 + wci * 16 + (lane & 15);
-  if (wk == 0) {
+  int hdr[KH], hdc[KH], hlo[KH];   // row / column relative to the tile origin (-1 .. 8)
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = co0 + wco * 32 + f * 16 + (lane >> 4) * 4 + r;
-          wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] =
-              F16 ? acc[f][tap][r] * (1.f / gsc) : acc[f][tap][r];
+  for (int k = 0; k < KH; ++k) {
+    const int pix = (tid + 256 * k) >> 3;
+    hdr[k] = pix < T::HALO ? pix / T::WP - 1 : -(1 << 20);   // dead item: never in range
+    hdc[k] = pix % T::WP - 1;
+    hlo[k] = pix * WGS_ASB + qh * 8;
+  }
+
+  float4 rg[KG], rh[KH];
+  float2 st_l[4], st_s[4];         // NORM: stats of the loading / the staging tile's image
+  int lb = 0, ly = 0, lx = 0;      // tile whose data the item registers receive
+  int sb = 0, sy = 0, sx = 0;      // tile being staged from them
+  auto tile_at = [&](int t, int& b0, int& y0, int& x0) EV_LAMBDA_INLINE {
+    const int ib = t / per_img, rr = t - ib * per_img, ty = rr / g.ntx;
+    b0 = ib; y0 = ty * T::TH; x0 = (rr - ty * g.ntx) * TW;
+  };
+  auto load_stats = [&]() EV_LAMBDA_INLINE {
+    if constexpr (NORM) {
+      const float2* sp = sstats + (size_t)lb * Cin + ci0 + qh * 4;
+      st_l[0] = sp[0]; st_l[1] = sp[1]; st_l[2] = sp[2]; st_l[3] = sp[3];
+    }
+  };
+  auto in_img = [&](int k, int y0, int x0) EV_LAMBDA_INLINE {
+    return (unsigned)(y0 + hdr[k]) < (unsigned)H && (unsigned)(x0 + hdc[k]) < (unsigned)W;
+  };
+  auto issue_item = [&](auto j_c) EV_LAMBDA_INLINE {
+    constexpr int j = decltype(j_c)::value;
+    if constexpr (j < KG) {
+      rg[j] = ld4(gy + ((size_t)lb * H + ly) * W * Cout + (size_t)lx * Cout + gyo[j]);
+    } else {
+      // unconditional, at a clamped address (the staging zeroes what lies outside the image):
+      // with every load issued, the compiler's vmcnt waits count exactly one tile's loads
+      constexpr int k = j - KG;
+      const int sh = min(max(UPS ? (ly >> 1) + (hdr[k] >> 1) : ly + hdr[k], 0), Hs - 1);
+      const int sw = min(max(UPS ? (lx >> 1) + (hdc[k] >> 1) : lx + hdc[k], 0), Ws - 1);
+      rh[k] = ld4(src + (((size_t)lb * Hs + sh) * Ws + sw) * Cin + ci0 + qh * 4);
+    }
+  };
+  float4 tb;   // this thread's gy sum of the staging tile (bias)
+  auto store_item = [&](auto j_c, char* buf) EV_LAMBDA_INLINE {
+    constexpr int j = decltype(j_c)::value;
+    if constexpr (j < KG) {
+      float4 v = rg[j];
+      tb.x += v.x; tb.y += v.y; tb.z += v.z; tb.w += v.w;
+      if constexpr (F16) v = make_float4(v.x * gsc, v.y * gsc, v.z * gsc, v.w * gsc);
+      store_pieces<NP>(buf + glo[j], GY_PIECE, v);
+    } else {
+      constexpr int k = j - KG;
+      if (hdr[k] > -2) {   // live item
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (in_img(k, sy, sx)) {
+          v = rh[k];
+          if (NORM)
+            v = make_float4(normact(v.x, st_s[0]), normact(v.y, st_s[1]), normact(v.z, st_s[2]),
+                            normact(v.w, st_s[3]));
         }
-  }
-  if (do_bias) {
-    double* xb = reinterpret_cast<double*>(wsm);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xb[i * 256 + tid] = bs[i];
-    __syncthreads();
-    if (tid < CO_T) {
-      const int qq = tid >> 2, i = tid & 3;
-      double sum = 0.0;
-      for (int m = qq; m < 256; m += QG) sum += xb[i * 256 + m];
-      bpart[(size_t)slice * Cout + co0 + tid] = (float)sum;
+        store_pieces<NP>(buf + NPC * GY_PIECE + hlo[k], ACT_PIECE, v);
+      }
     }
+  };
+  auto all_items = [&](auto fn) EV_LAMBDA_INLINE { static_for<NIT>(fn); };
+  auto shift = [&]() EV_LAMBDA_INLINE {   // the loaded tile becomes the staging tile
+    sb = lb; sy = ly; sx = lx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st_s[i] = st_l[i];
+  };
+
+  // per-lane transposed-read geometry (wgrad_split_kernel)
+  const int gq = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+  const int acol = (wco * 32 + 4 * p4) * 2;
+  const int bcol = (wci * 16 + 4 * p4) * 2;
+
+  if (t_beg < t_end) {
+    // prologue: tile t_beg staged into set 0, tile t_beg+1 (clamped) in the registers
+    tile_at(t_beg, lb, ly, lx);
+    load_stats();
+    all_items([&](auto j) EV_LAMBDA_INLINE { issue_item(j); });
+    shift();
+    tb = make_float4(0.f, 0.f, 0.f, 0.f);
+    all_items([&](auto j) EV_LAMBDA_INLINE { store_item(j, wsm); });
+    bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
+    tile_at(min(t_beg + 1, t_end - 1), lb, ly, lx);
+    load_stats();
+    all_items([&](auto j) EV_LAMBDA_INLINE { issue_item(j); });
   }
+  __syncthreads();
+  for (int t = t_beg; t < t_end; ++t) {
+    const int cur = (t - t_beg) & 1;
+    const char* gimg = wsm + cur * BUF;
+    const char* aimg = gimg + NPC * GY_PIECE;
+    char* nbuf = wsm + (1 - cur) * BUF;
+    // the registers hold tile t+1: staged into the other set during this tile (surplus
+    // copies of the last tile land in a set nobody reads), refilled with tile t+2
+    shift();
+    tile_at(min(t + 2, t_end - 1), lb, ly, lx);
+    load_stats();
+    tb = make_float4(0.f, 0.f, 0.f, 0.f);
+    static_for<KSTEPS / KSPLIT>([&](auto si_c) EV_LAMBDA_INLINE {
+      constexpr int si = decltype(si_c)::value;
+      const int s = wk + si * KSPLIT;
+      const int px0 = 32 * s + 4 * gq + q, px1 = px0 + 16;
+      bf16x8w a[NPC][2];
+#pragma unroll
+      for (int i = 0; i < NPC; ++i)
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+          a[i][f] = tr_frag(gimg + i * GY_PIECE + px0 * GSB + acol + f * 32,
+                            gimg + i * GY_PIECE + px1 * GSB + acol + f * 32);
+      const int hp0 = (px0 / TW) * T::WP + px0 % TW, hp1 = (px1 / TW) * T::WP + px1 % TW;
+      static_for<9>([&](auto tap_c) EV_LAMBDA_INLINE {
+        constexpr int tap = decltype(tap_c)::value;
+        constexpr int toff = (tap / 3) * T::WP + tap % 3;
+        bf16x8w b[NPC];
+#pragma unroll
+        for (int i = 0; i < NPC; ++i)
+          b[i] = tr_frag(aimg + i * ACT_PIECE + (hp0 + toff) * WGS_ASB + bcol,
+                         aimg + i * ACT_PIECE + (hp1 + toff) * WGS_ASB + bcol);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          f32x4 c = acc[f][tap];
+#ifdef EV_WGP_NOMFMA   // timing experiment only (wrong results)
+          c[0] += (float)a[0][f][0] * (float)b[0][0] + (float)a[1][f][1] * (float)b[1][1];
+#else
+          c = mfma16_piece<NP>(a[1][f], b[0], c);
+          c = mfma16_piece<NP>(a[0][f], b[1], c);
+          c = mfma16_piece<NP>(a[0][f], b[0], c);
+#endif
+          acc[f][tap] = c;
+        }
+        // this slot's share of the staging: item j at slot j * NSLOT / NIT
+        all_items([&](auto j_c) EV_LAMBDA_INLINE {
+          constexpr int j = decltype(j_c)::value;
+#ifndef EV_WGP_NOSTAGE   // timing experiment only (wrong results)
+          if constexpr (si * 9 + tap == (j * NSLOT) / NIT) {
+            store_item(j_c, nbuf);
+            issue_item(j_c);
+          }
+#endif
+        });
+      });
+    });
+    if (t + 1 < t_end) {
+      bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
+    }
+    __syncthreads();
+  }
+  wgrad_split_finish<NWCO, KSPLIT, F16>(acc, bs, wsm, wpart, bpart, slice, co0, ci0, Cin, Cout, gsc,
+                                        ci0 == 0);
 }
 
 // ------------------------------------------------------------------ cin == 1 (first conv)
@@ -964,6 +1249,47 @@ static void launch_wgs(dim3 grid, hipStream_t s, const float* src, const float* 
     launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 8, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT);
 }
 
+template <int NP, int NWCO, int KSPLIT, int MODE>
+static void launch_wgp(dim3 grid, hipStream_t s, const float* src, const float* st, const float* gy,
+                       float* wpart, float* bpart, int B, int H, int W, int cin, int cout,
+                       const WgGeom& g, const float* gmax, int gmT) {
+  constexpr int CO_T = NWCO * 32;
+  const size_t lds_img = 2 * (size_t)npc(NP) * ((size_t)64 * (CO_T * 2 + 32) + (size_t)100 * WGS_ASB);
+  const size_t lds_fold = KSPLIT == 2 ? (size_t)2 * 72 * 64 * 4 : 0;
+  size_t lds = lds_img;
+  if (lds < lds_fold) lds = lds_fold;
+  if (lds < 256 * 4 * 8) lds = 256 * 4 * 8;
+  auto k = wgrad_pipe_kernel<NP, NWCO, KSPLIT, MODE>;
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, (const float2*)st, gy, wpart, bpart, B, H, W,
+                     cin, cout, g, gmax, gmT);
+}
+
+template <int NP>
+static void dispatch_wgp(int mode, bool narrow, dim3 grid, hipStream_t s, const float* src,
+                         const float* st, const float* gy, float* wpart, float* bpart, int B, int H,
+                         int W, int cin, int cout, const WgGeom& g, const float* gmax, int gmT) {
+  if (narrow) {
+    switch (mode) {
+      case ACT_RAW: launch_wgp<NP, 1, 2, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_NORM: launch_wgp<NP, 1, 2, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_UP: launch_wgp<NP, 1, 2, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      default: launch_wgp<NP, 1, 2, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+    }
+  } else {
+    switch (mode) {
+      case ACT_RAW: launch_wgp<NP, 2, 1, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_NORM: launch_wgp<NP, 2, 1, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_UP: launch_wgp<NP, 2, 1, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      default: launch_wgp<NP, 2, 1, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+    }
+  }
+}
+
 template <int NP>
 static void dispatch_wgs(int mode, bool narrow, dim3 grid, hipStream_t s, const float* src,
                          const float* st, const float* gy, float* wpart, float* bpart, int B, int H,
@@ -1001,6 +1327,7 @@ extern "C" int ebsdvae_conv3x3_wgrad_split_slices(int B, int H, int W, int cin, 
   WgGeom g;
   if (pieces != 2 && pieces != 3 && pieces != NP_F16) return -1;
   if (cin % 32 || !(cout == 32 || cout % 64 == 0)) return -1;
+  if (pieces != 3 && wg_pipe()) return wg_pipe_geom(B, H, W, cin, cout, &g) ? g.slices : -1;
   const int pt = 64;
   if (!wg_geom(B, H, W, cin, cout, &g, pt) || !wgs_geom_ok(g, pt)) return -1;
   return g.slices;
@@ -1019,10 +1346,17 @@ extern "C" int ebsdvae_conv3x3_wgrad_split(const float* src, const float* src_st
   EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats, "conv3x3_wgrad_split: NORM needs stats");
   EV_REQUIRE(cin % 32 == 0 && (cout == 32 || cout % 64 == 0), "conv3x3_wgrad_split: cin=%d cout=%d unsupported",
              cin, cout);
+  hipStream_t s = (hipStream_t)stream;
+  if (pieces == 2 && wg_pipe()) {
+    EV_REQUIRE(wg_pipe_geom(B, H, W, cin, cout, &g), "conv3x3_wgrad_split: unsupported shape H=%d W=%d", H, W);
+    const bool narrow = cout == 32;
+    dispatch_wgp<2>(src_mode, narrow, wg_pipe_grid(g, cin, cout), s, src, src_stats, gy, wpart, bpart, B,
+                    H, W, cin, cout, g, nullptr, 0);
+    return evh::check_launch("wgrad_split");
+  }
   const int pt = 64;   // 64-pixel tiles: the per-piece LDS images and prefetch registers fit
   EV_REQUIRE(wg_geom(B, H, W, cin, cout, &g, pt) && wgs_geom_ok(g, pt),
              "conv3x3_wgrad_split: unsupported shape H=%d W=%d", H, W);
-  hipStream_t s = (hipStream_t)stream;
   // 32-wide co tiles where the 64-wide variant would exceed 256 VGPRs
   const bool narrow = cout == 32 || g.TW == 8 || (pieces == 3 && g.TW == 16);
   const dim3 grid(g.slices, narrow ? cout / 32 : cout / 64, cin / 32);
@@ -1048,6 +1382,13 @@ extern "C" int ebsdvae_conv3x3_wgrad_f16(const float* src, const float* src_stat
   EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats, "conv3x3_wgrad_f16: NORM needs stats");
   EV_REQUIRE(cin % 32 == 0 && (cout == 32 || cout % 64 == 0), "conv3x3_wgrad_f16: cin=%d cout=%d unsupported",
              cin, cout);
+  if (wg_pipe()) {
+    EV_REQUIRE(wg_pipe_geom(B, H, W, cin, cout, &g), "conv3x3_wgrad_f16: unsupported shape H=%d W=%d", H, W);
+    const bool narrow = cout == 32;
+    dispatch_wgp<NP_F16>(src_mode, narrow, wg_pipe_grid(g, cin, cout), (hipStream_t)stream, src, src_stats,
+                         gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gm_tiles);
+    return evh::check_launch("wgrad_f16");
+  }
   const int pt = 64;
   EV_REQUIRE(wg_geom(B, H, W, cin, cout, &g, pt) && wgs_geom_ok(g, pt),
              "conv3x3_wgrad_f16: unsupported shape H=%d W=%d", H, W);
