@@ -113,7 +113,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // (f16_wshift, stored in the pack's trailer); gradient operands are scaled by a power of two
 // from their maximum (f16_shift) so that both sit inside fp16's range.
 constexpr int NP_F16 = 16;   // == EBSDVAE_PIECES_F16
-constexpr int kF16PackTrailer = 16;   // bytes after the split-fp16 pack: int32 weight shift k
+// bytes after the split-fp16 pack: int32 weight shift k (16-byte head), then the
+// kF16MaxParts partial maxima of |w| it is computed from (pack_wmax_kernel)
+constexpr int kF16MaxParts = 64;
+constexpr int kF16PackTrailer = 16 + 4 * kF16MaxParts;
 constexpr int npc(int np) { return np == NP_F16 ? 2 : np; }   // pieces per operand
 
 // Two floats -> their split-fp16 pieces, packed: hi = (f16(a), f16(b)) round-to-nearest

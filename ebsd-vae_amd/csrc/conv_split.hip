@@ -67,10 +67,12 @@ EV_DEVINL void split_bf16(float x, __bf16 (&p)[NP]) {
 // and the three products a0b0 + a0b1 + a1b0 on v_mfma_f32_32x32x16_f16 (the dropped a1b1 is
 // <= 2^-24 relative): ~2^-22.5 per product, at the bf16x3 rate.  fp16's range is narrow, so
 // the weights of each layer are packed as w * 2^k, k from the layer's max |w| (max |w| 2^k in
-// [2^11, 2^12): pack_wshift_kernel, stored in the pack's trailer) and the epilogue multiplies
-// the accumulators by the exact 2^-k.  Forward operands are normalised activations
-// (IN + LeakyReLU, |x| <= sqrt(H*W) by construction), which fp16 holds as they are; the
-// gradient operand of input-gradient launches is scaled per image from its maxima (GS).
+// [2^11, 2^12): pack_wmax_kernel + pack_split_kernel, stored in the pack's trailer) and the
+// epilogue multiplies the accumulators by the exact 2^-k.  Forward operands are normalised
+// activations (IN + LeakyReLU, |x| <= sqrt(H*W - 1) by construction), which fp16 holds as
+// they are; the gradient operand of input-gradient launches is scaled per image by a power of
+// two from its per-tile maxima (GS), and so is the weight gradient's per slice
+// (conv_wgrad.hip).
 
 template <int NP>
 EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
@@ -969,13 +971,14 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #endif
 }
 
-// NP_F16 packs: the layer's weight shift k = f16_shift_of(max |w|) into the pack's trailer
-// (one block per layer; runs before pack_split_kernel on the same stream)
-__global__ __launch_bounds__(256) void pack_wshift_kernel(const PackBatch pb) {
-  const ebsdvae_pack_desc& q = pb.d[blockIdx.x];
+// NP_F16 packs, step 1: partial maxima of |w| per layer, kF16MaxParts blocks per layer, into
+// the pack's trailer after its 16-byte head (grid (kF16MaxParts, layers); runs before
+// pack_split_kernel on the same stream)
+__global__ __launch_bounds__(256) void pack_wmax_kernel(const PackBatch pb) {
+  const ebsdvae_pack_desc& q = pb.d[blockIdx.y];
   const int n = q.cin * q.cout * 9;
   float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(q.src[i]));
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += kF16MaxParts * 256) m = fmaxf(m, fabsf(q.src[i]));
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
   __shared__ float wm[4];
   if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
@@ -983,9 +986,8 @@ __global__ __launch_bounds__(256) void pack_wshift_kernel(const PackBatch pb) {
   if (threadIdx.x == 0) {
     const int ci_ = q.for_dgrad ? q.cout : q.cin, co_ = q.for_dgrad ? q.cin : q.cout;
     const size_t body = (size_t)(ci_ / XCK) * XTAPS * npc(NP_F16) * co_ * XCK * 2;
-    const float mx = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
-    *reinterpret_cast<int4*>(reinterpret_cast<char*>(q.dst) + body) =
-        make_int4(mx > 0.f ? f16_shift_of(mx) : 0, 0, 0, 0);   // the whole 16-byte trailer
+    float* parts = reinterpret_cast<float*>(reinterpret_cast<char*>(q.dst) + body + 16);
+    parts[blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
   }
 }
 
@@ -998,6 +1000,18 @@ __global__ void pack_split_kernel(const PackBatch pb, int np) {
   const int nch = ci_ / XCK;
   const int n = nch * XTAPS * co_ * XCK;
   __bf16* d = reinterpret_cast<__bf16*>(q.dst);
+  // NP_F16: the layer's weight shift k = f16_shift_of(max |w|) from the partial maxima in the
+  // trailer (every block reduces them; block 0 writes k into the 16-byte head, which no block
+  // reads, so the order of the blocks does not matter)
+  int k16 = 0;
+  if (np == NP_F16) {
+    const float* parts = reinterpret_cast<const float*>(d + (size_t)n * npc(np)) + 4;
+    float m = 0.f;
+    for (int i = 0; i < kF16MaxParts; ++i) m = fmaxf(m, parts[i]);
+    k16 = m > 0.f ? f16_shift_of(m) : 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      *reinterpret_cast<int4*>(d + (size_t)n * npc(np)) = make_int4(k16, 0, 0, 0);
+  }
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int c8 = e % XCK;
     int r = e / XCK;
@@ -1016,8 +1030,7 @@ __global__ void pack_split_kernel(const PackBatch pb, int np) {
     }
     const size_t base = ((size_t)(chunk * XTAPS + t) * npc(np)) * co_ * XCK + (size_t)o * XCK + c8;
     if (np == NP_F16) {   // two fp16 pieces of the scaled weight (conv3x3_pipe_kernel undoes it)
-      const int k = *reinterpret_cast<const int*>(d + (size_t)n * npc(np));   // trailer
-      const float ws = ldexpf(w, k);
+      const float ws = ldexpf(w, k16);
       const _Float16 h0 = (_Float16)ws;
       const _Float16 h1 = (_Float16)(ws - (float)h0);
       d[base] = __builtin_bit_cast(__bf16, h0);
@@ -1258,7 +1271,7 @@ extern "C" int ebsdvae_pack_conv_weights_split(const ebsdvae_pack_desc* descs, i
   int bx = (maxn + 255) / 256;
   if (bx > 64) bx = 64;
   if (pieces == NP_F16)
-    hipLaunchKernelGGL(pack_wshift_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, pb);
+    hipLaunchKernelGGL(pack_wmax_kernel, dim3(kF16MaxParts, n), dim3(256), 0, (hipStream_t)stream, pb);
   hipLaunchKernelGGL(pack_split_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, pb, pieces);
   return evh::check_launch("pack_conv_weights_split");
 }

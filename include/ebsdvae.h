@@ -105,8 +105,9 @@ int ebsdvae_conv3x3_cout1_dgrad(const float* g, const float* w, float* gin, int 
  *   pieces = 3 ("bf16x6", 6 MFMAs, ~2^-25: fp32 grade);
  *   pieces = EBSDVAE_PIECES_F16 ("f16x3": two fp16 pieces x0 = f16(x), x1 = f16(x - x0) on
  *     v_mfma_f32_32x32x16_f16, 3 MFMAs, ~2^-22.5 per product; the pack holds w * 2^k with one
- *     power of two per layer, max |w| 2^k in [2^11, 2^12), k in a 16-byte trailer that
- *     ebsdvae_pack_split_bytes includes, so any weight magnitude keeps fp16's full precision).
+ *     power of two per layer, max |w| 2^k in [2^11, 2^12), k in a trailer that
+ *     ebsdvae_pack_split_bytes includes (int32 k in its 16-byte head, then 64 partial maxima
+ *     of |w| it is reduced from), so any weight magnitude keeps fp16's full precision).
  * Weights use the split pack ([cin'/8][tap 0..9][piece][cout'][8] bf16,
  * ebsdvae_pack_split_bytes bytes).  Shapes: ebsdvae_conv3x3_split_supported; InstanceNorm
  * partials use ebsdvae_conv3x3_split_stat_tiles tiles per image.  pmode = -1 in
