@@ -149,6 +149,9 @@ struct InBwdFuse {
   float* ypool = nullptr;   // FP_POOLOUT forward: the max-pooled raw output
   const float* gmax = nullptr;   // NP_F16 input gradient: per-tile max |g| (B, gmT)
   int gmT = 0;
+  float2* st_out = nullptr;      // in-kernel InstanceNorm finalize (pipe_owns_images): forward
+  float2* bst_out = nullptr;     // {mean, rstd}, or the previous block's backward {m1, m2}
+  double inv_hw = 0.0;           // 1 / (H*W) of the previous block (bst_out)
 };
 
 }  // namespace ev

@@ -22,6 +22,7 @@
 //   LDS weight slab per chunk: [tap 0..9][piece][Cout][8 ch] bf16, DMA'd by global_load_lds
 //     from the split pack (ebsdvae_pack_conv_weights_split).
 #include "conv_common.h"
+#include "instnorm_fin.h"
 
 #include <stdlib.h>
 #include <type_traits>
@@ -517,7 +518,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
     float* __restrict__ act_out, int B, int H, int W, int Cin, int TH, int tpb,
     const float* __restrict__ yprev, const float2* __restrict__ stprev, double2* __restrict__ ipart,
-    float* __restrict__ ypool, const float* __restrict__ gmax, int gmT) {
+    float* __restrict__ ypool, const float* __restrict__ gmax, int gmT, float2* __restrict__ st_out,
+    float2* __restrict__ bst_out, double fin_inv_hw) {
   constexpr int WN = NWV / WM;
   constexpr int NT = WN * NF * 32;               // == Cout
   constexpr int MW = MF * 32;
@@ -961,6 +963,30 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     zero_acc();
     EV_TACC(tr_epi, te0);
   }
+  // InstanceNorm finalize of the images this block owns (the host passes st_out / bst_out
+  // only when every block's tile run covers whole images, pipe_owns_images): the forward
+  // {mean, rstd} from this conv's statistics partials, or the previous block's backward
+  // {m1, m2} from the fused reduce's partials, as the standalone finalize kernels compute them
+  if (st_out || bst_out) {
+    // the surplus weight DMA of the last iterations still targets LDS, which the finalize
+    // reuses; the epilogue stores of every wave must be visible to the whole block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __threadfence_block();
+    __syncthreads();
+    const int tpi = NI == 1 ? H / TH : 1;
+    const int g0 = t0 / tpi, g1 = (t0 + ntl - 1) / tpi;
+    for (int gi = g0; gi <= g1; ++gi)
+      for (int im = 0; im < NI; ++im) {
+        const int b = gi * NI + im;
+        if (b >= B) break;
+        if (st_out)
+          in_stats_finalize_image(spart, st_out, NT, (H * W) / MW, (float)MW, b, tid,
+                                  reinterpret_cast<float*>(xsm));
+        if (bst_out)
+          in_bwd_finalize_image(ipart, bst_out, NT, (H * W) / MW, fin_inv_hw, b, tid,
+                                reinterpret_cast<double*>(xsm));
+      }
+  }
 #ifdef EV_PIPE_TRACE
   if (lane == 0 && blockIdx.x < 4096) {
     unsigned long long* o = ev_pipe_trace + ((size_t)blockIdx.x * 8 + (wave & 7)) * 6;
@@ -1127,6 +1153,24 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   return c->lds <= 160 * 1024;
 }
 
+// Does the persistent kernel's tile split give every block whole images (t0 = blockIdx.x * tpb
+// on an image boundary, tpb a multiple of the tiles per image), so that each block can run the
+// InstanceNorm finalize of its own images after its last tile?  (B = 256 at 128^2: 32 tiles of
+// 4 rows per image, 8192 tiles over 256 CUs -> exactly one image per block.)
+// EBSDVAE_FUSE_FINALIZE=0 always takes the standalone finalize kernels (A/B, tests).
+static bool pipe_owns_images(const X3Cfg& c, int B, int H) {
+  static const bool on = [] {
+    const char* e = getenv("EBSDVAE_FUSE_FINALIZE");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || !(c.NI > 1 || (use_pipe() && c.lds_pipe))) return false;
+  const int tpi = c.NI > 1 ? 1 : H / c.TH;
+  const int ntiles = ((B + c.NI - 1) / c.NI) * tpi;
+  const int ncu = cu_count();
+  const int tpb = (ntiles + ncu - 1) / ncu;
+  return tpb % tpi == 0;
+}
+
 template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI>
 static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const void* wp,
                         const float* bias, float* y, float* part, float* aout, int B, int H, int W,
@@ -1145,7 +1189,7 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
     const int nblk = (ntiles + tpb - 1) / tpb;
     hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), c.lds_pipe, s, src, (const float2*)st,
                        (const char*)wp, bias, y, (float2*)part, aout, B, H, W, cin, c.TH, tpb, f.yprev,
-                       f.stprev, f.part, f.ypool, f.gmax, f.gmT);
+                       f.stprev, f.part, f.ypool, f.gmax, f.gmT, f.st_out, f.bst_out, f.inv_hw);
     return;
   }
   if constexpr (NI == 1 && FP != FP_POOLOUT && NP != NP_F16) {
@@ -1368,4 +1412,74 @@ extern "C" int ebsdvae_conv3x3_dgrad_inbwd_f16(const float* g, const float* gmax
   dispatch_split(c, NP_F16, g, nullptr, ACT_RAW, wpack, nullptr, gin, nullptr, nullptr, B, H, W, cin,
                  cout, (hipStream_t)stream, pmode, f);
   return evh::check_launch("conv3x3_dgrad_inbwd_f16");
+}
+
+// Forward split conv + its InstanceNorm statistics st (B, cout) {mean, rstd}: finalized by the
+// conv's own blocks when they own whole images (pipe_owns_images), otherwise by the standalone
+// finalize kernel after it; bit-identical either way.  ypool != NULL: the pooled producer form.
+extern "C" int ebsdvae_conv3x3_fwd_split_st(const float* src, const float* src_stats, int src_mode,
+                                            const void* wpack, const float* bias, float* y,
+                                            float* ypool, float* stat_part, float* st, int B,
+                                            int H, int W, int cin, int cout, int pieces,
+                                            ebsdvae_stream_t stream) {
+  X3Cfg c;
+  EV_REQUIRE(src && wpack && y && stat_part && st && B > 0,
+             "conv3x3_fwd_split_st: null pointer or empty batch");
+  EV_REQUIRE(src_mode >= 0 && src_mode <= 4, "conv3x3_fwd_split_st: bad src_mode %d", src_mode);
+  EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats,
+             "conv3x3_fwd_split_st: NORM modes need src_stats");
+  EV_REQUIRE(!ypool || (src_mode == ACT_NORM && ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, pieces)),
+             "conv3x3_fwd_split_st: pooled output unsupported for H=%d W=%d src_mode=%d", H, W, src_mode);
+  EV_REQUIRE(plan_split(H, W, cin, cout, pieces, &c),
+             "conv3x3_fwd_split_st: unsupported shape H=%d W=%d cin=%d cout=%d pieces=%d", H, W, cin,
+             cout, pieces);
+  const bool fused = pipe_owns_images(c, B, H);
+  InBwdFuse f;
+  f.ypool = ypool;
+  if (fused) f.st_out = (float2*)st;
+  dispatch_split(c, pieces, src, src_stats, src_mode, wpack, bias, y, stat_part, nullptr, B, H, W,
+                 cin, cout, (hipStream_t)stream, -1, f);
+  if (int rc = evh::check_launch("conv3x3_fwd_split_st")) return rc;
+  if (fused) return 0;
+  const int T = ebsdvae_conv3x3_split_stat_tiles(H, W, cout);
+  return ebsdvae_in_stats_finalize(stat_part, st, B, cout, T, (H * W) / T, stream);
+}
+
+// ebsdvae_conv3x3_dgrad_inbwd_f16 with a fused reduce (pmode >= 0) that also returns the
+// previous block's finalized InstanceNorm-backward statistics bst (B, cin) over prev_hw pixels
+// (what ebsdvae_in_bwd_finalize makes of part), in-kernel where pipe_owns_images allows.
+extern "C" int ebsdvae_conv3x3_dgrad_inbwd_f16_bst(const float* g, const float* gmax, int gm_tiles,
+                                                   const void* wpack, float* gin, const float* y_prev,
+                                                   const float* st_prev, int pmode, double* part,
+                                                   float* bst, int prev_hw, int B, int H, int W,
+                                                   int cin, int cout, ebsdvae_stream_t stream) {
+  X3Cfg c;
+  EV_REQUIRE(g && gmax && gm_tiles > 0 && wpack && gin && B > 0,
+             "conv3x3_dgrad_inbwd_f16_bst: null pointer, empty batch or no gradient maxima");
+  EV_REQUIRE(pmode >= 0 && pmode <= P_UPSUM && y_prev && st_prev && part && bst && prev_hw > 0 &&
+                 (W & (W - 1)) == 0,
+             "conv3x3_dgrad_inbwd_f16_bst: fused reduce needs pmode >= 0, y_prev, st_prev, part, bst, "
+             "prev_hw and W = 2^k");
+  EV_REQUIRE(pmode != P_UPSUM || ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, NP_F16),
+             "conv3x3_dgrad_inbwd_f16_bst: summed upsample adjoint unsupported for H=%d W=%d", H, W);
+  EV_REQUIRE(plan_split(H, W, cin, cout, NP_F16, &c),
+             "conv3x3_dgrad_inbwd_f16_bst: unsupported shape H=%d W=%d cin=%d cout=%d", H, W, cin, cout);
+  const bool fused = pipe_owns_images(c, B, H);
+  InBwdFuse f;
+  f.yprev = y_prev;
+  f.stprev = (const float2*)st_prev;
+  f.part = (double2*)part;
+  f.gmax = gmax;
+  f.gmT = gm_tiles;
+  if (fused) {
+    f.bst_out = (float2*)bst;
+    f.inv_hw = 1.0 / (double)prev_hw;
+  }
+  dispatch_split(c, NP_F16, g, nullptr, ACT_RAW, wpack, nullptr, gin, nullptr, nullptr, B, H, W, cin,
+                 cout, (hipStream_t)stream, pmode, f);
+  if (int rc = evh::check_launch("conv3x3_dgrad_inbwd_f16_bst")) return rc;
+  if (fused) return 0;
+  // (cin, cout) are the conv's: gin and the previous block have cout channels
+  return ebsdvae_in_bwd_finalize(part, bst, B, cout, ebsdvae_conv3x3_split_stat_tiles(H, W, cout), prev_hw,
+                                 stream);
 }

@@ -12,50 +12,17 @@
 // two HBM-bound passes (reduce, apply) over NHWC planes with float4 channel vectors; the
 // plane sums use fixed-order two-level reductions (deterministic).
 #include "common.h"
+#include "instnorm_fin.h"
 #include "../../include/ebsdvae.h"
 
 namespace ev {
 
-// One workgroup per pattern b: thread (c = tid % C, j = tid / C) folds tiles j, j+J, ... of
-// channel c (coalesced over c), then lane j == 0 folds the J partial results in order.
-// All tiles hold n elements, so the Chan merge reduces to: mean = avg(mean_t),
-// M2 = sum(M2_t) + n * sum((mean_t - mean)^2).
+// One workgroup per pattern b (in_stats_finalize_image, instnorm_fin.h).
 __global__ __launch_bounds__(256) void in_stats_finalize_kernel(const float2* __restrict__ part,
                                                                 float2* __restrict__ st, int C,
                                                                 int T, float n) {
-  __shared__ float sm[3][256];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int J = 256 / C;
-  const int c = tid % C, j = tid / C;
-  const float2* p = part + (size_t)b * T * C + c;
-  float m = 0.f;
-  int cnt = 0;
-#pragma unroll 8
-  for (int t = j; t < T; t += J) { m += p[(size_t)t * C].x; ++cnt; }
-  sm[0][tid] = m;
-  sm[1][tid] = (float)cnt;
-  __syncthreads();
-  float mean = 0.f;
-  for (int k = 0; k < J; ++k) mean += sm[0][k * C + c];
-  mean /= (float)T;
-  float m2 = 0.f, dm = 0.f;
-#pragma unroll 8
-  for (int t = j; t < T; t += J) {
-    const float2 v = p[(size_t)t * C];
-    m2 += v.y;
-    const float d = v.x - mean;
-    dm = fmaf(d, d, dm);
-  }
-  __syncthreads();
-  sm[0][tid] = m2;
-  sm[2][tid] = dm;
-  __syncthreads();
-  if (j == 0) {
-    float a = 0.f, q = 0.f;
-    for (int k = 0; k < J; ++k) { a += sm[0][k * C + c]; q += sm[2][k * C + c]; }
-    const float var = (a + n * q) / (n * (float)T);
-    st[(size_t)b * C + c] = make_float2(mean, 1.0f / sqrtf(var + kInEps));
-  }
+  __shared__ float sm[3 * 256];
+  in_stats_finalize_image(part, st, C, T, n, blockIdx.x, threadIdx.x, sm);
 }
 
 __global__ void act_apply_kernel(const float* __restrict__ src, const float2* __restrict__ st,
@@ -247,33 +214,12 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
   }
 }
 
-// One workgroup per pattern b (C <= 256): thread (c = tid % C, j = tid / C) sums tiles
-// j, j+J, ... of channel c in double, then lane j == 0 folds the J sums in order.
+// One workgroup per pattern b (in_bwd_finalize_image, instnorm_fin.h).
 __global__ __launch_bounds__(256) void in_bwd_finalize_kernel(const double2* __restrict__ part,
                                                               float2* __restrict__ bst, int C,
                                                               int T, double inv_hw) {
-  __shared__ double sm[2][256];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int J = 256 / C;
-  const int c = tid % C, j = tid / C;
-  const double2* p = part + (size_t)b * T * C + c;
-  double s1 = 0.0, s2 = 0.0;
-  if (j < J) {
-#pragma unroll 8
-    for (int t = j; t < T; t += J) {
-      const double2 v = p[(size_t)t * C];
-      s1 += v.x;
-      s2 += v.y;
-    }
-  }
-  sm[0][tid] = s1;
-  sm[1][tid] = s2;
-  __syncthreads();
-  if (j == 0) {
-    double a = 0.0, q = 0.0;
-    for (int k = 0; k < J; ++k) { a += sm[0][k * C + c]; q += sm[1][k * C + c]; }
-    bst[(size_t)b * C + c] = make_float2((float)(a * inv_hw), (float)(q * inv_hw));
-  }
+  __shared__ double sm[2 * 256];
+  in_bwd_finalize_image(part, bst, C, T, inv_hw, blockIdx.x, threadIdx.x, sm);
 }
 
 // ------------------------------------------------------------------ network-end fusions

@@ -400,21 +400,26 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     flops = conv_flops(B, H, H, layer.cin, layer.cout)
     nb = 4 * (src.numel() + y.numel() + (y.numel() // 4 if pool_out else 0))   # algorithmic I/O
     ypool = None
+    st = _empty(B, layer.cout, 2, like=w)
     if pool_out:
         ypool = _empty(B, H // 2, H // 2, layer.cout, like=w)
-        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split_pooled", N.ptr(src),
+    if wp.pieces and not keep_act:
+        # conv + InstanceNorm statistics finalize (in-kernel where the blocks own whole images)
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split_st", N.ptr(src),
                 N.ptr(src_stats), src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y), N.ptr(ypool),
-                N.ptr(part), B, H, H, layer.cin, layer.cout, wp.pieces, N.stream(), tag=tag + " pool",
-                pieces=wp.pieces, nbytes=nb)
-    elif wp.pieces:
-        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split", *args, wp.pieces,
-                N.stream(), tag=tag, pieces=wp.pieces, nbytes=nb)
+                N.ptr(part), N.ptr(st), B, H, H, layer.cin, layer.cout, wp.pieces, N.stream(),
+                tag=tag + (" pool" if pool_out else ""), pieces=wp.pieces, nbytes=nb)
     else:
-        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", *args, N.stream(), tag=tag,
-                nbytes=nb)
-    st = _empty(B, layer.cout, 2, like=w)
-    N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
-           N.stream())
+        if pool_out:
+            raise ValueError("conv_forward: pool_out needs a split pack and no keep_act")
+        if wp.pieces:
+            _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd_split", *args, wp.pieces,
+                    N.stream(), tag=tag, pieces=wp.pieces, nbytes=nb)
+        else:
+            _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_fwd", *args, N.stream(), tag=tag,
+                    nbytes=nb)
+        N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
+               N.stream())
     if pool_out:
         return y, st, ypool
     if keep_act:
@@ -433,9 +438,10 @@ def in_backward(gnext, pmode, y, st, part=None):
         part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
         N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), part.data_ptr(),
                B, H, W, C, s)
-    T = part.shape[1]
-    bst = _empty(B, C, 2, like=y)
-    N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, T, H * W, s)
+    bst = getattr(part, "ev_bst", None)   # finalized by the fused input-gradient conv
+    if bst is None:
+        bst = _empty(B, C, 2, like=y)
+        N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, part.shape[1], H * W, s)
     gy = torch.empty_like(y)
     if _FWD_PIECES.get(_PRECISION):
         # per-tile max |gy|: the scale of the split-fp16 input-gradient conv that consumes gy
@@ -451,6 +457,9 @@ def in_backward(gnext, pmode, y, st, part=None):
 
 
 def _in_bwd_stats(B, C, T, HW, part, like):
+    bst = getattr(part, "ev_bst", None)   # finalized by the fused input-gradient conv
+    if bst is not None:
+        return bst
     bst = _empty(B, C, 2, like=like)
     N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, T, HW, N.stream())
     return bst
@@ -663,20 +672,23 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
         if gmax is None:
             raise RuntimeError("conv_dgrad: split-fp16 input gradient needs gy's per-tile maxima "
                                "(in_backward under f16x3)")
-        part = None
         if prev is None:
-            yp = sp = pptr = None
-            pmode = -1
-        else:
-            y_prev, st_prev, pmode = prev
-            T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, W, layer.cin)
-            part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
-            yp, sp, pptr = N.ptr(y_prev), N.ptr(st_prev), part.data_ptr()
-        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_f16", N.ptr(gy),
-                N.ptr(gmax), gmax.shape[1], N.ptr(wd.t), N.ptr(gin), yp, sp, pmode, pptr, B, H, W,
-                layer.cout, layer.cin, N.stream(), tag=tag + ("" if prev is None else " +inbwd"),
-                pieces=wd.pieces, nbytes=nbd)
-        return gin if prev is None else (gin, part)
+            _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_f16", N.ptr(gy),
+                    N.ptr(gmax), gmax.shape[1], N.ptr(wd.t), N.ptr(gin), None, None, -1, None, B, H,
+                    W, layer.cout, layer.cin, N.stream(), tag=tag, pieces=wd.pieces, nbytes=nbd)
+            return gin
+        # fused reduce + finalize of the previous block's InstanceNorm backward: part carries
+        # the finalized statistics (part.ev_bst) for in_backward / in_backward_first
+        y_prev, st_prev, pmode = prev
+        T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, W, layer.cin)
+        part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
+        bst = _empty(B, layer.cin, 2, like=gy)
+        _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_f16_bst", N.ptr(gy),
+                N.ptr(gmax), gmax.shape[1], N.ptr(wd.t), N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev),
+                pmode, part.data_ptr(), N.ptr(bst), y_prev.shape[1] * y_prev.shape[2], B, H, W,
+                layer.cout, layer.cin, N.stream(), tag=tag + " +inbwd", pieces=wd.pieces, nbytes=nbd)
+        part.ev_bst = bst
+        return gin, part
     if prev is None:
         if wd.pieces:
             _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_split", N.ptr(gy),

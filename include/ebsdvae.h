@@ -154,6 +154,28 @@ int ebsdvae_conv3x3_dgrad_inbwd_f16(const float* g, const float* gmax, int gm_ti
                                     const void* wpack, float* gin, const float* y_prev,
                                     const float* st_prev, int pmode, double* part, int B, int H,
                                     int W, int cin, int cout, ebsdvae_stream_t stream);
+/* The same launches with the InstanceNorm finalize folded in (one launch where the
+ * persistent kernel's blocks each own whole images, e.g. B = 256 at 128x128 -- then every
+ * block finalizes its own images after its last tile -- else the conv followed by the
+ * standalone finalize; bit-identical either way, EBSDVAE_FUSE_FINALIZE=0 forces the latter):
+ *   _fwd_split_st: ebsdvae_conv3x3_fwd_split (ypool = NULL) or _fwd_split_pooled (ypool set),
+ *     then ebsdvae_in_stats_finalize(stat_part, st, B, cout, tiles, H*W/tiles) -> st (B, cout)
+ *     {mean, rstd};
+ *   _dgrad_inbwd_f16_bst: ebsdvae_conv3x3_dgrad_inbwd_f16 with pmode >= 0, then
+ *     ebsdvae_in_bwd_finalize(part, bst, B, cout, tiles, prev_hw) -> bst (B, cout), with
+ *     (cin, cout) the channels of g and gin as in ebsdvae_conv3x3_dgrad_inbwd_f16 and prev_hw
+ *     the H*W of y_prev.
+ * Replace the conv + finalize pairs of the training step (latice/model.py:95-97 forward,
+ * their autograd backward). */
+int ebsdvae_conv3x3_fwd_split_st(const float* src, const float* src_stats, int src_mode,
+                                 const void* wpack, const float* bias, float* y, float* ypool,
+                                 float* stat_part, float* st, int B, int H, int W, int cin,
+                                 int cout, int pieces, ebsdvae_stream_t stream);
+int ebsdvae_conv3x3_dgrad_inbwd_f16_bst(const float* g, const float* gmax, int gm_tiles,
+                                        const void* wpack, float* gin, const float* y_prev,
+                                        const float* st_prev, int pmode, double* part, float* bst,
+                                        int prev_hw, int B, int H, int W, int cin, int cout,
+                                        ebsdvae_stream_t stream);
 
 /* ---- weight gradients (deterministic two-level reduction) -----------------------------
  * Partial dW[co][ci][tap] and db[co] over pixel slices; then ebsdvae_wgrad_reduce sums

@@ -40,7 +40,10 @@ def test_two_rank_gradient_equals_single_process(cuda, tmp_path, prec):
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_trainer_worker.py")],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = [p.communicate(timeout=150)[0].decode() for p in procs]
-    assert all(p.returncode == 0 for p in procs), outs
+    for p, out in zip(procs, outs):   # the tail of a failing worker's output, untruncated
+        if p.returncode != 0:
+            print(out[-6000:])
+    assert all(p.returncode == 0 for p in procs), [o[-300:] for o in outs]
     from latice import engine as E
     with E.precision(prec):
         m = VariationalAutoEncoderRawData()

@@ -763,3 +763,76 @@ def test_f16_weight_pack_trailer_and_batch(cuda):
             if pd is not None:
                 single = E.pack_weight(w, L, dgrad=True, scaled=True)
                 assert pd.pieces == single.pieces and torch.equal(pd.t, single.t), L.name
+
+
+@pytest.mark.parametrize("B,H,cin,cout,mode", [(3, 16, 128, 128, 1), (5, 8, 128, 128, 1),
+                                               (256, 32, 64, 128, 2), (2, 128, 32, 32, 1)])
+def test_fused_stats_finalize_bitwise(cuda, B, H, cin, cout, mode):
+    """ebsdvae_conv3x3_fwd_split_st == ebsdvae_conv3x3_fwd_split + ebsdvae_in_stats_finalize
+    bit for bit, whether the persistent blocks finalize their own images in-kernel (16x16,
+    8x8 two-image tiles, B=256 at 32x32) or the standalone kernel runs (B=2 at 128x128)."""
+    rng = np.random.default_rng(83 + B + H)
+    s, mean, rstd, st = make_src(rng, B, H, cin, mode)
+    w = dev(rng.standard_normal((cout, cin, 3, 3)) * 0.05)
+    b = dev(rng.standard_normal(cout) * 0.1)
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, mode, 0)
+    with E.precision("f16x3"):
+        wp = E.pack_weight(w, layer, dgrad=False)
+    assert wp.pieces == E.PIECES_F16
+    src, sst = dev(s), dev(st)
+    T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, H, cout)
+    outs = []
+    for fused in (True, False):
+        y = torch.empty(B, H, H, cout, device=cuda)
+        part = torch.empty(B, T, cout, 2, device=cuda)
+        stt = torch.full((B, cout, 2), float("nan"), device=cuda)
+        if fused:
+            N.call("ebsdvae_conv3x3_fwd_split_st", N.ptr(src), N.ptr(sst), mode, N.ptr(wp.t), N.ptr(b),
+                   N.ptr(y), None, N.ptr(part), N.ptr(stt), B, H, H, cin, cout, wp.pieces, N.stream())
+        else:
+            N.call("ebsdvae_conv3x3_fwd_split", N.ptr(src), N.ptr(sst), mode, N.ptr(wp.t), N.ptr(b),
+                   N.ptr(y), N.ptr(part), None, B, H, H, cin, cout, wp.pieces, N.stream())
+            N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(stt), B, cout, T, (H * H) // T,
+                   N.stream())
+        outs.append((y, stt))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])   # no NaN left: every image finalized
+
+
+@pytest.mark.parametrize("B,H,cin,cout,pmode", [(3, 16, 128, 128, 0), (256, 32, 64, 128, 1),
+                                                (2, 128, 32, 32, 0), (4, 32, 128, 128, 2)])
+def test_fused_bwd_finalize_bitwise(cuda, B, H, cin, cout, pmode):
+    """ebsdvae_conv3x3_dgrad_inbwd_f16_bst == ebsdvae_conv3x3_dgrad_inbwd_f16 +
+    ebsdvae_in_bwd_finalize bit for bit (gin, the reduce partials and bst), in-kernel
+    (16x16; B=256 at 32x32 with the max-pool routing) and standalone (B=2 at 128x128)."""
+    rng = np.random.default_rng(89 + B + H + pmode)
+    Hp = {0: H, 1: 2 * H, 2: H // 2}[pmode]   # the previous block's resolution
+    gy = rng.standard_normal((B, H, H, cout)).astype(np.float32)
+    yp = rng.standard_normal((B, Hp, Hp, cin)).astype(np.float32)
+    stp = np.stack([yp.mean(axis=(1, 2)), 1.0 / np.sqrt(yp.var(axis=(1, 2)) + 1e-5)], -1)
+    w = dev(rng.standard_normal((cout, cin, 3, 3)) * 0.05)
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, 1, 0)
+    with E.precision("f16x3"):
+        wd = E.pack_weight(w, layer, dgrad=True, scaled=True)
+    assert wd.pieces == E.PIECES_F16
+    g, y_prev, st_prev = dev(gy), dev(yp), dev(stp)
+    gmax = g.abs().reshape(B, 4, -1).amax(2).contiguous()
+    T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, H, cin)
+    outs = []
+    for fused in (True, False):
+        gin = torch.empty(B, H, H, cin, device=cuda)
+        part = torch.empty(B, T, cin, 2, dtype=torch.float64, device=cuda)
+        bst = torch.full((B, cin, 2), float("nan"), device=cuda)
+        if fused:
+            N.call("ebsdvae_conv3x3_dgrad_inbwd_f16_bst", N.ptr(g), N.ptr(gmax), 4, N.ptr(wd.t),
+                   N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev), pmode, part.data_ptr(), N.ptr(bst),
+                   Hp * Hp, B, H, H, cout, cin, N.stream())
+        else:
+            N.call("ebsdvae_conv3x3_dgrad_inbwd_f16", N.ptr(g), N.ptr(gmax), 4, N.ptr(wd.t), N.ptr(gin),
+                   N.ptr(y_prev), N.ptr(st_prev), pmode, part.data_ptr(), B, H, H, cout, cin, N.stream())
+            N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, cin, T, Hp * Hp, N.stream())
+        outs.append((gin, part, bst))
+    torch.cuda.synchronize()
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_)
