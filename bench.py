@@ -402,8 +402,10 @@ def main():
         if probe is not None and i % args.probe_every == 0:
             # event-bracketed launches on a sample of the timed steps: each event pair costs
             # the stream a few microseconds, so bracketing every launch of every step would
-            # slow the step the value is quoted on by ~2 %
-            with probe:
+            # slow the step the value is quoted on by ~2 %.  These steps keep the weight
+            # gradients on the main stream, so that every launch is timed alone (overlapped
+            # launches would each carry the other's time); ~1.4 % slower, one step in five
+            with probe, E.serial_streams():
                 out = trainer.step(x)
             probed += 1
         else:
@@ -461,11 +463,13 @@ def main():
                       " product, fp32 accumulation)",
             "bf16x3": " (2 bf16 pieces, 3 products: ~2^-16.5 per product)",
             "f16x3": " (fp32 operands split into 2 fp16 pieces, 3 fp16 MFMA products per fp32"
-                     " product, ~2^-22.5, fp32 accumulation: forward convs with weights packed x256;"
-                     " input-gradient and weight-gradient convs with the gradient operand scaled"
-                     " by a power of two per image / per slice; fp32 MFMA for the 1->32 and 8x8"
-                     " layers where f16 is not supported; all activations, statistics and"
-                     " reductions fp32/fp64; passes the fp32 parity gates, tests/test_gpu_trainer.py)"}[prec],
+                     " product, ~2^-22.5, fp32 accumulation: forward, input-gradient and"
+                     " weight-gradient convs; weights packed as w*2^k with one power of two per"
+                     " layer from max|w|, the gradient operand scaled by a power of two per image"
+                     " (input gradient) or per slice (weight gradient); fp32 MFMA for the 1->32"
+                     " conv, bf16x6 for the 8x8 weight gradient fed by an upsample; all"
+                     " activations, statistics and reductions fp32/fp64; passes the fp32 parity"
+                     " gates, tests/test_gpu_trainer.py)"}[prec],
         "config": {"workload": f"c{2 if world == 1 else 3}: VariationalAutoEncoderRawData "
                                f"{args.image_size}x{args.image_size}, latent {args.latent_dim}, "
                                f"batch {args.batch}/GPU, fwd+loss+bwd+Adam"

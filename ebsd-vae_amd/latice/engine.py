@@ -476,8 +476,24 @@ _WG_STREAM = os.environ.get("EBSDVAE_WGRAD_STREAM", "1") != "0"
 _SIDE = {}
 
 
+_SERIAL = 0   # > 0 inside serial_streams()
+
+
+@contextlib.contextmanager
+def serial_streams():
+    """Keep the weight gradients on the current stream (no overlap), e.g. while per-launch
+    durations are being measured: overlapped launches would each be timed with the other's
+    work inside (bench.py's probed steps)."""
+    global _SERIAL
+    _SERIAL += 1
+    try:
+        yield
+    finally:
+        _SERIAL -= 1
+
+
 def _side_stream(device):
-    if not _WG_STREAM or torch.cuda.is_current_stream_capturing():
+    if not _WG_STREAM or _SERIAL or torch.cuda.is_current_stream_capturing():
         return None
     key = device.index if device.index is not None else torch.cuda.current_device()
     if key not in _SIDE:
