@@ -239,21 +239,24 @@ def _empty(*shape, like):
 
 
 # ----------------------------------------------------------------------------- precision
-# Conv arithmetic (csrc/conv_fwd.hip, csrc/conv_split.hip):
+# Conv arithmetic (csrc/conv_fwd.hip, csrc/conv_split.hip, csrc/conv_wgrad.hip):
 #   "fp32"   v_mfma_f32_32x32x2_f32 (exact fp32 products);
 #   "bf16x6" 3-piece split-bf16 MFMA, 6 products per fp32 product (~2^-25, fp32 grade);
 #   "bf16x3" 2-piece split-bf16 MFMA, 3 products (~2^-16.5 per product);
-#   "f16x3"  forward and input-gradient convs on 2-piece split-fp16 MFMA (x0 = f16(x),
-#            x1 = f16(x - x0); weights packed x256; the gradient operand of each image scaled
-#            by a power of two from the max |gy| the InstanceNorm-backward apply emits),
-#            3 products (~2^-22.5 per product); weight gradients on bf16x6.
-# Split modes cover every conv layer the split kernel supports (Cout in {32,64,128},
-# H*W >= 256, plus the 8x8 maps for bf16x6); the others stay fp32.
+#   "f16x3"  2-piece split-fp16 MFMA (x0 = f16(x), x1 = f16(x - x0)), 3 products (~2^-22.5
+#            per product) for the forward, input-gradient and weight-gradient convs: weights
+#            packed as w * 2^k with one power of two per layer from max |w| (pack trailer),
+#            the gradient operand scaled by a power of two per image (input gradient) or per
+#            slice (weight gradient) from the per-tile max |gy| the InstanceNorm-backward apply
+#            emits; where a layer has no fp16 kernel (8x8 weight gradient of an upsampled
+#            source) it takes bf16x6.
+# Split modes cover every conv layer the split kernels support (Cout in {32,64,128},
+# H*W >= 256, plus the 8x8 maps); the others (the 1->32 first conv) stay fp32.
 PIECES_F16 = 16   # EBSDVAE_PIECES_F16 (include/ebsdvae.h)
 _PIECES = {"fp32": 0, "bf16x3": 2, "bf16x6": 3, "f16x3": 3}
 _FWD_PIECES = {"f16x3": PIECES_F16}   # forward-conv piece format where it differs
-# default: f16x3 (forward) + bf16x6 (gradients); passes every fp32 parity gate
-# (tests/test_gpu_model.py runs fp32, bf16x6 and f16x3)
+# default: f16x3; passes every fp32 parity gate (tests/test_gpu_model.py and
+# tests/test_gpu_trainer.py run fp32, bf16x6 and f16x3)
 _PRECISION = os.environ.get("EBSDVAE_PRECISION", "f16x3")
 if _PRECISION not in _PIECES:
     raise ValueError(f"EBSDVAE_PRECISION must be one of {sorted(_PIECES)}")

@@ -41,8 +41,9 @@ def h(t):
 def prec(request):
     """The model-level gates hold for the fp32-grade split-bf16 convs, the pure fp32-MFMA
     convs AND split-fp16 (f16x3, the default).  Under f16x3 this autograd path runs the
-    split-fp16 forward and the f16 weight gradient; its input gradients use the unscaled
-    pack (bf16x6 dgrad) -- the trainer's f16 dgrad is pinned in test_gpu_trainer.py."""
+    split-fp16 forward, input gradient (gy carries its per-tile maxima, so each call packs
+    the scaled dgrad weights) and weight gradient; the trainer's batched-pack path, the
+    one bench.py times, is pinned in test_gpu_trainer.py."""
     from latice import engine as E
     with E.precision(request.param):
         yield request.param
