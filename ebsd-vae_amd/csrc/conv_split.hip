@@ -343,7 +343,10 @@ EV_DEVINL void pipe_barrier() {
 // with 32-bit buffer offsets instead of 64-bit addresses (the same values, the same
 // summation order, so results are bit-identical to the non-persistent kernel's).
 //   wpx0  tile pixel of the wave's first fragment, mfs the pixel stride between its fragments
-//         (32: one contiguous run; W: FP_POOLOUT's row pairs), slot its statistics slot
+//         (32: one contiguous run; W: FP_POOLOUT's / FP_UPSUM's row pairs), slot the
+//         statistics slot of its first 64 pixels: the wave's MF fragments form MF / 2 groups
+//         of two (64 pixels) and every group writes one {mean, M2} (spart) or one fused-reduce
+//         double2 (ipart) slot, so every configuration has (H*W)/64 slots per image
 //   ypool FP_POOLOUT: the (H/2, W/2) max-pooled raw output (2x2 windows are lane-local)
 template <int MF, int NF, int FP, int NT>
 EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bias,
@@ -351,8 +354,9 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
                              int h0, int wpx0, int mfs, int slot, int co_base, int hk, int l32,
                              const float* __restrict__ yprev, const float2* __restrict__ stprev,
                              double2* __restrict__ ipart, float* __restrict__ ypool) {
-  constexpr int MW = MF * 32;
-  const int T = (H * W) / MW;
+  static_assert(MF % 2 == 0, "fragments in 64-pixel pairs");
+  constexpr int NG = MF / 2;
+  const int T = (H * W) / 64;
   const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ((size_t)b0 * H + h0) * W * NT), 0,
                                                     0x7fffffff, 0x00020000);
 #pragma unroll
@@ -360,14 +364,16 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
     const int co = co_base + nf * 32 + l32;
     const float bb = bias ? bias[co] : 0.f;
     const int vbase = ((wpx0 + 4 * hk) * NT + co) * 4;
-    float s = 0.f;
+    float s[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) s[g] = 0.f;
 #pragma unroll
     for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float v = acc[mf][nf][r] + bb;
         acc[mf][nf][r] = v;
-        s += v;
+        s[mf >> 1] += v;
         if (FP != FP_UPSUM)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
                                                 vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
@@ -376,72 +382,77 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
       // y is (B, H/2, W/2, NT): the 2x2 sums of this conv's output (the upsample adjoint),
       // and the previous block (at H/2) is reduced once per window:
       // sum_window(g) * lrelu'(xhat) == sum_window(g * lrelu'(xhat)), xhat constant on it
-      static_assert(MF == 2, "row-pair fragments");
       const int W2 = W >> 1;
       const auto rq = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(y + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
       const auto rp = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(yprev + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
       const float2 sp = stprev[(size_t)b0 * NT + co];
-      float gs[8], v[8];
-      int off[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        int prow, pc;
-        if (W >= 32) {   // fragment 0 = row 2rp, fragment 1 = row 2rp + 1, same 32 columns
-          const int r = 2 * k;
-          gs[k] = (acc[0][nf][r] + acc[0][nf][r + 1]) + (acc[1][nf][r] + acc[1][nf][r + 1]);
-          prow = wpx0 / W >> 1;
-          pc = ((wpx0 % W + 4 * hk) >> 1) + (((r & 3) + 8 * (r >> 2)) >> 1);
-        } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
-          const int mf = k >> 2, r = 2 * (k & 3);
-          gs[k] = (acc[mf][nf][r] + acc[mf][nf][r + 1]) + (acc[mf][nf][r + 8] + acc[mf][nf][r + 9]);
-          prow = (wpx0 + mf * mfs) / W >> 1;
-          pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
+      for (int g = 0; g < NG; ++g) {
+        const int m0 = 2 * g;   // the group's fragment pair
+        float gs[8], v[8];
+        int off[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          int prow, pc;
+          if (W >= 32) {   // fragment m0 = row 2rp, fragment m0 + 1 = row 2rp + 1, same 32 columns
+            const int r = 2 * k;
+            gs[k] = (acc[m0][nf][r] + acc[m0][nf][r + 1]) + (acc[m0 + 1][nf][r] + acc[m0 + 1][nf][r + 1]);
+            prow = (wpx0 / W + m0) >> 1;
+            pc = ((wpx0 % W + 4 * hk) >> 1) + (((r & 3) + 8 * (r >> 2)) >> 1);
+          } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
+            const int mf = m0 + (k >> 2), r = 2 * (k & 3);
+            gs[k] = (acc[mf][nf][r] + acc[mf][nf][r + 1]) + (acc[mf][nf][r + 8] + acc[mf][nf][r + 9]);
+            prow = (wpx0 + mf * mfs) / W >> 1;
+            pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
+          }
+          off[k] = ((prow * W2 + pc) * NT + co) * 4;
         }
-        off[k] = ((prow * W2 + pc) * NT + co) * 4;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, 0));
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, gs[k]), rq, off[k], 0, 0);
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) inbwd_acc<P_ID>(gs[k], &v[k], sp, s1, s2);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (hk == 0) ipart[((size_t)b0 * T + slot + g) * NT + co] = make_double2((double)s1, (double)s2);
       }
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, 0));
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, gs[k]), rq, off[k], 0, 0);
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) inbwd_acc<P_ID>(gs[k], &v[k], sp, s1, s2);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (hk == 0) ipart[((size_t)b0 * T + slot) * NT + co] = make_double2((double)s1, (double)s2);
     }
     if (FP == FP_POOLOUT) {
       // max(lrelu(IN(y))) over a window == lrelu(IN(max y)) (IN's scale is positive, both maps
       // are monotone), so the consumer reads this tensor in ACT_NORM mode with y's statistics
-      static_assert(MF == 2, "row-pair fragments");
       const int W2 = W >> 1;
       const auto rq = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(ypool + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
-      if (W >= 32) {   // fragment 0 = tile row 2rp, fragment 1 = row 2rp + 1, same 32 columns
-        const int prow = wpx0 / W >> 1, pcol = (wpx0 % W + 4 * hk) >> 1;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const float m = fmaxf(fmaxf(acc[0][nf][r], acc[0][nf][r + 1]),
-                                fmaxf(acc[1][nf][r], acc[1][nf][r + 1]));
-          const int pc = pcol + (((r & 3) + 8 * (r >> 2)) >> 1);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
-                                                ((prow * W2 + pc) * NT + co) * 4, 0, 0);
-        }
-      } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
+      for (int m0 = 0; m0 < MF; m0 += 2) {
+        if (W >= 32) {   // fragment m0 = tile row 2rp, fragment m0 + 1 = row 2rp + 1, same 32 columns
+          const int prow = (wpx0 / W + m0) >> 1, pcol = (wpx0 % W + 4 * hk) >> 1;
 #pragma unroll
-        for (int mf = 0; mf < 2; ++mf) {
-          const int prow = (wpx0 + mf * mfs) / W >> 1;
-#pragma unroll
-          for (int r = 0; r < 8; r += 2) {
-            const float m = fmaxf(fmaxf(acc[mf][nf][r], acc[mf][nf][r + 1]),
-                                  fmaxf(acc[mf][nf][r + 8], acc[mf][nf][r + 9]));
-            const int pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
+          for (int r = 0; r < 16; r += 2) {
+            const float m = fmaxf(fmaxf(acc[m0][nf][r], acc[m0][nf][r + 1]),
+                                  fmaxf(acc[m0 + 1][nf][r], acc[m0 + 1][nf][r + 1]));
+            const int pc = pcol + (((r & 3) + 8 * (r >> 2)) >> 1);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
                                                   ((prow * W2 + pc) * NT + co) * 4, 0, 0);
+          }
+        } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
+#pragma unroll
+          for (int mf = m0; mf < m0 + 2; ++mf) {
+            const int prow = (wpx0 + mf * mfs) / W >> 1;
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+              const float m = fmaxf(fmaxf(acc[mf][nf][r], acc[mf][nf][r + 1]),
+                                    fmaxf(acc[mf][nf][r + 8], acc[mf][nf][r + 9]));
+              const int pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
+                                                    ((prow * W2 + pc) * NT + co) * 4, 0, 0);
+            }
           }
         }
       }
@@ -449,50 +460,57 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
     if (FP != FP_NONE && FP != FP_POOLOUT && FP != FP_UPSUM) {
       constexpr int NL = FP == P_POOL ? 4 : 1;
       constexpr int GM = NF == 1 ? 32 : EV_PIPE_EPI_G;   // loads in flight per batch
-      constexpr int G = (GM / NL) < MF * 16 ? (GM / NL) : MF * 16;
-      static_assert((MF * 16) % G == 0, "batch size");
+      constexpr int G = (GM / NL) < 32 ? (GM / NL) : 32;
+      static_assert(32 % G == 0, "batches stay inside one 64-pixel group");
       const int lW = 31 - __builtin_clz(W);
       const int plane = FP == P_POOL ? 4 * H * W : (FP == P_UP ? (H * W) / 4 : H * W);
       const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)(yprev + (size_t)b0 * plane * NT), 0,
                                                         plane * NT * 4, 0x00020000);
       const float2 sp = stprev[(size_t)b0 * NT + co];
       const int pbase = h0 * W + wpx0 + 4 * hk;
-      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int e0 = 0; e0 < MF * 16; e0 += G) {
-        float v[G][NL];
+      for (int g = 0; g < NG; ++g) {
+        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const int e = e0 + j, mf = e >> 4, r = e & 15;
-          const int pl = pbase + mf * 32 + (r & 3) + 8 * (r >> 2);
+        for (int e0 = 32 * g; e0 < 32 * g + 32; e0 += G) {
+          float v[G][NL];
 #pragma unroll
-          for (int k = 0; k < NL; ++k)
-            v[j][k] = __builtin_bit_cast(
-                float, __builtin_amdgcn_raw_buffer_load_b32(rp, (inbwd_pix<FP>(pl, W, lW, k) * NT + co) * 4, 0, 0));
+          for (int j = 0; j < G; ++j) {
+            const int e = e0 + j, mf = e >> 4, r = e & 15;
+            const int pl = pbase + mf * 32 + (r & 3) + 8 * (r >> 2);
+#pragma unroll
+            for (int k = 0; k < NL; ++k)
+              v[j][k] = __builtin_bit_cast(
+                  float, __builtin_amdgcn_raw_buffer_load_b32(rp, (inbwd_pix<FP>(pl, W, lW, k) * NT + co) * 4, 0, 0));
+          }
+#pragma unroll
+          for (int j = 0; j < G; ++j) {
+            const int e = e0 + j;
+            inbwd_acc<FP>(acc[e >> 4][nf][e & 15], v[j], sp, s1, s2);
+          }
         }
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const int e = e0 + j;
-          inbwd_acc<FP>(acc[e >> 4][nf][e & 15], v[j], sp, s1, s2);
-        }
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (hk == 0) ipart[((size_t)b0 * T + slot + g) * NT + co] = make_double2((double)s1, (double)s2);
       }
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (hk == 0) ipart[((size_t)b0 * T + slot) * NT + co] = make_double2((double)s1, (double)s2);
     }
     if (spart) {
-      s += __shfl_xor(s, 32, 64);
-      const float mean = s * (1.0f / MW);
-      float q = 0.f;
 #pragma unroll
-      for (int mf = 0; mf < MF; ++mf)
+      for (int g = 0; g < NG; ++g) {
+        float sg = s[g];
+        sg += __shfl_xor(sg, 32, 64);
+        const float mean = sg * (1.0f / 64);
+        float q = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float d = acc[mf][nf][r] - mean;
-          q = fmaf(d, d, q);
-        }
-      q += __shfl_xor(q, 32, 64);
-      if (hk == 0) spart[((size_t)b0 * T + slot) * NT + co] = make_float2(mean, q);
+        for (int mf = 2 * g; mf < 2 * g + 2; ++mf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float d = acc[mf][nf][r] - mean;
+            q = fmaf(d, d, q);
+          }
+        q += __shfl_xor(q, 32, 64);
+        if (hk == 0) spart[((size_t)b0 * T + slot + g) * NT + co] = make_float2(mean, q);
+      }
     }
   }
 }
@@ -561,7 +579,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   int fpx0 = wm * MW, mfs = 32;
   if ((FP == FP_POOLOUT || FP == FP_UPSUM) && W >= 32) {
     const int cbs = W >> 5, rp = wm / cbs;
-    fpx0 = 2 * rp * W + (wm - rp * cbs) * 32;
+    fpx0 = MF * rp * W + (wm - rp * cbs) * 32;   // rows MF*rp .. MF*rp + MF-1 (pairs)
     mfs = W;
   }
   int abase[MF];
@@ -784,7 +802,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     }
     if (NI == 1 || b0 + im < B)
       pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
-                                    (h0 * W + wm * MW - im * tpx) / MW, wn * NF * 32, hk, l32,
+                                    (h0 * W + wm * MW - im * tpx) / 64, wn * NF * 32, hk, l32,
                                     yprev, stprev, ipart, ypool);
   };
 
@@ -817,7 +835,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     // are issued before the MFMAs of k-step s, so only k-step 0 waits on an LDS latency.
     // NF > 1 has twice the MFMAs per k-step to cover the reads and no VGPRs to spare for a
     // second set (it would spill): one set, read at the start of each k-step
-    constexpr bool FPF = NF == 1;
+    constexpr bool FPF = NF == 1 && MF <= 2;   // MF = 4 has no VGPRs for a second set
     bf16x8 fa[FPF ? 2 : 1][NPC][MF], fb[FPF ? 2 : 1][NPC][NF];
     auto load_frags = [&](int s, bf16x8 (&a)[NPC][MF], bf16x8 (&b)[NPC][NF]) EV_LAMBDA_INLINE {
 #pragma unroll
@@ -980,10 +998,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
         const int b = gi * NI + im;
         if (b >= B) break;
         if (st_out)
-          in_stats_finalize_image(spart, st_out, NT, (H * W) / MW, (float)MW, b, tid,
+          in_stats_finalize_image(spart, st_out, NT, (H * W) / 64, 64.f, b, tid,
                                   reinterpret_cast<float*>(xsm));
         if (bst_out)
-          in_bwd_finalize_image(ipart, bst_out, NT, (H * W) / MW, fin_inv_hw, b, tid,
+          in_bwd_finalize_image(ipart, bst_out, NT, (H * W) / 64, fin_inv_hw, b, tid,
                                 reinterpret_cast<double*>(xsm));
       }
   }
@@ -1288,7 +1306,7 @@ extern "C" int ebsdvae_conv3x3_split_supported(int H, int W, int cin, int cout, 
 
 extern "C" int ebsdvae_conv3x3_split_stat_tiles(int H, int W, int cout) {
   (void)cout;
-  return (H * W) / 64;   // every split configuration has 64-pixel wave tiles
+  return (H * W) / 64;   // every split configuration writes one statistics slot per 64 pixels
 }
 
 extern "C" size_t ebsdvae_pack_split_bytes(int cin, int cout, int pieces) {
