@@ -1100,6 +1100,15 @@ static bool use_pipe() {
 }
 
 // EBSDVAE_CONV_MULTI_IMAGE=0: 8x8 maps go to the fp32 small-map kernels (A/B timing)
+// EBSDVAE_CONV_SMALL1=0: the 8x8 split-fp16 convs keep two-image tiles (A/B)
+static bool use_small_one_image() {
+  static const bool v = [] {
+    const char* e = getenv("EBSDVAE_CONV_SMALL1");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 static bool use_multi_image() {
   static const int v = [] {
     const char* e = getenv("EBSDVAE_CONV_MULTI_IMAGE");
@@ -1148,6 +1157,13 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
     c->M = 128;
     c->NI = 2;
     c->TH = H;
+    if (np == NP_F16 && use_small_one_image()) {
+      // split-fp16: one image per block and 4 waves of 64 px x 32 co, so that B = 256 gives
+      // 256 blocks (two-image tiles fill only half the CUs)
+      c->M = 64;
+      c->NI = 1;
+      c->nwv = 4;
+    }
   } else {
     if (W > c->M || c->M % W) return false;
     c->TH = c->M / W;
@@ -1268,6 +1284,8 @@ static void dispatch_split(const X3Cfg& c, int np, const float* src, const float
   } else if (np == NP_F16) {
     if (cout == 128 && c.NI > 1)   // two 8x8 images per tile
       launch_x3<NP_F16, 8, 2, 2, 1, 1, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else if (cout == 128 && c.M == 64)   // one 8x8 image per tile, 4 waves
+      launch_x3<NP_F16, 4, 1, 2, 1, 1>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 128)
       launch_x3<NP_F16, 8, 4, 2, 2, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 64)

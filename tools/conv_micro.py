@@ -32,6 +32,8 @@ CASES = {
     "fwd64pool": ("fwdpool", 64, 64, 64, ACT_NORM),
     "fwd128pool": ("fwdpool", 32, 128, 128, ACT_NORM),
     "fwd32to64n": ("fwd", 64, 32, 64, ACT_NORM),
+    "fwd128s8": ("fwd", 8, 128, 128, ACT_NORM),
+    "dgrad128s8": ("dgrad", 8, 128, 128, P_ID),
     "dgrad32": ("dgrad", 128, 32, 32, P_ID),
     "dgrad64": ("dgrad", 64, 64, 64, P_ID),
     "dgrad32u": ("dgrad", 128, 32, 32, P_UP),
