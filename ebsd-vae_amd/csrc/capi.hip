@@ -29,3 +29,39 @@ int check_launch(const char* what) {
 
 extern "C" const char* ebsdvae_last_error(void) { return g_err; }
 extern "C" int ebsdvae_version(void) { return 1; }
+
+// ------------------------------------------------------------------ cross-stream ordering
+// `waiter` waits for the work enqueued on `signaler` so far, through an event recorded with a
+// device-scope release (hipEventReleaseToDevice) instead of the default system-scope fence:
+// both streams run on this device, so nothing needs to become visible to the host, and the
+// system-scope writeback + invalidate of every fork / join costs the GPU a few microseconds of
+// idle time (tools/step_gaps.py).  A wait takes the event's state at enqueue time, so a small
+// ring of events per device is reused round-robin; capturable into hipGraphs (fork / join).
+extern "C" int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler) {
+  constexpr int kRing = 64, kMaxDev = 64;
+  static hipEvent_t ring[kMaxDev][kRing];
+  static int next[kMaxDev];
+  static bool made[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
+    evh::set_error("stream_wait: no current device");
+    return 2;
+  }
+  if (!made[dev]) {
+    for (int i = 0; i < kRing; ++i)
+      if (hipEventCreateWithFlags(&ring[dev][i], hipEventDisableTiming | hipEventReleaseToDevice) !=
+          hipSuccess) {
+        evh::set_error("stream_wait: hipEventCreateWithFlags failed");
+        return 2;
+      }
+    made[dev] = true;
+  }
+  hipEvent_t ev = ring[dev][next[dev]];
+  next[dev] = (next[dev] + 1) % kRing;
+  if (hipEventRecord(ev, (hipStream_t)signaler) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)waiter, ev, 0) != hipSuccess) {
+    evh::set_error("stream_wait: %s", hipGetErrorString(hipGetLastError()));
+    return 2;
+  }
+  return 0;
+}

@@ -25,6 +25,7 @@ F = ctypes.c_float
 SIGNATURES = {
     "ebsdvae_last_error": [],
     "ebsdvae_version": [],
+    "ebsdvae_stream_wait": [P, P],
     "ebsdvae_pack_conv_weight": [P, P, I, I, I, I, P],
     "ebsdvae_pack_conv_weights": [P, I, P],
     "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, P, I, I, I, I, I, P],

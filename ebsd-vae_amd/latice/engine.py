@@ -472,11 +472,20 @@ def _in_bwd_stats(B, C, T, HW, part, like):
 # Weight gradients are off the backward's critical path (in_backward -> input gradient -> ...):
 # they run on a second HIP stream, so they overlap the memory-bound InstanceNorm-backward passes
 # and the other kernels' tails.  The side stream waits for the main stream before each weight
-# gradient (its inputs are ready), the slice reductions run on the main stream after joining
-# it; record_stream keeps the caching allocator from recycling a buffer one stream still uses.
+# gradient (its inputs are ready), and the batched slice reductions run on the side stream too,
+# behind the weight gradients they sum.  The main stream waits for the side stream once, at
+# the next join: at the end of a batched_wgrad_reduce() block, or -- inside
+# deferred_side_join() (the trainer's backward) -- only when that block exits.
+# Buffers the side stream touches are kept alive on the host until that join (no
+# record_stream: its event records on every free cost the GPU idle time at each join).
 # EBSDVAE_WGRAD_STREAM=0 keeps everything on the current stream.
 _WG_STREAM = os.environ.get("EBSDVAE_WGRAD_STREAM", "1") != "0"
+# Inside a hipGraph capture the side stream forks from and joins back into the capturing
+# stream (event edges in the graph).  EBSDVAE_GRAPH_SIDE=0 captures on one stream instead.
+_GRAPH_SIDE = os.environ.get("EBSDVAE_GRAPH_SIDE", "1") != "0"
 _SIDE = {}
+_KEEP = {}    # device -> buffers the side stream uses, released at the join (None: not in use)
+_DEFER = 0    # > 0 inside deferred_side_join()
 
 
 _SERIAL = 0   # > 0 inside serial_streams()
@@ -495,19 +504,74 @@ def serial_streams():
         _SERIAL -= 1
 
 
-def _side_stream(device):
-    if not _WG_STREAM or _SERIAL or torch.cuda.is_current_stream_capturing():
-        return None
-    key = device.index if device.index is not None else torch.cuda.current_device()
+def _dev_key(device):
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def side_stream(device):
+    """The weight-gradient side stream of `device` (created on first use)."""
+    key = _dev_key(device)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=device)
     return _SIDE[key]
 
 
+def _side_stream(device):
+    if not _WG_STREAM or _SERIAL:
+        return None
+    if not _GRAPH_SIDE and torch.cuda.is_current_stream_capturing():
+        return None
+    return side_stream(device)
+
+
+# EBSDVAE_LIGHT_EVENTS=0: fork / join through torch's Stream.wait_stream (system-scope fence)
+_LIGHT_EVENTS = os.environ.get("EBSDVAE_LIGHT_EVENTS", "1") != "0"
+
+
+def stream_wait(waiter, signaler):
+    """`waiter` (a torch Stream) waits for the work enqueued on `signaler` so far."""
+    if _LIGHT_EVENTS:
+        N.call("ebsdvae_stream_wait", waiter.cuda_stream, signaler.cuda_stream)
+    else:
+        waiter.wait_stream(signaler)
+
+
+def _side_use(device, *tensors):
+    """Fork the side stream from the current stream and keep `tensors` alive until the join."""
+    key = _dev_key(device)
+    side = side_stream(device)
+    stream_wait(side, torch.cuda.current_stream(device))
+    keep = _KEEP.get(key)
+    if keep is None:
+        keep = _KEEP[key] = []
+    keep.extend(t for t in tensors if t is not None)
+    return side
+
+
+def _side_pending(device) -> bool:
+    return _KEEP.get(_dev_key(device)) is not None
+
+
 def _join_side(device):
-    side = _SIDE.get(device.index if device.index is not None else torch.cuda.current_device())
-    if side is not None:
-        torch.cuda.current_stream(device).wait_stream(side)
+    """The current stream waits for the side stream's work so far; the buffers it used are
+    released (any later use of them is ordered behind this wait)."""
+    key = _dev_key(device)
+    if _KEEP.get(key) is not None:   # only a side stream that took work since the last join
+        stream_wait(torch.cuda.current_stream(device), _SIDE[key])
+        _KEEP[key] = None
+
+
+@contextlib.contextmanager
+def deferred_side_join(device):
+    """Batched reductions inside the block leave their results on the side stream; the
+    current stream joins it once, when the block exits."""
+    global _DEFER
+    _DEFER += 1
+    try:
+        yield
+    finally:
+        _DEFER -= 1
+        _join_side(device)
 
 
 # Weight-gradient slice reductions queued inside `batched_wgrad_reduce()` run as ONE batched
@@ -529,31 +593,44 @@ def batched_wgrad_reduce():
 
 
 def _flush_reduces(q):
-    if q:
-        _join_side(q[0][0].device)
-    for i in range(0, len(q), N.MAX_WGRAD_BATCH):
-        chunk = q[i:i + N.MAX_WGRAD_BATCH]
-        descs = (N.WgradReduceDesc * len(chunk))(*[
-            N.WgradReduceDesc(N.ptr(wp), N.ptr(bp), N.ptr(dw), N.ptr(db), S_, cin, cout, kind)
-            for wp, bp, S_, cin, cout, kind, dw, db in chunk])
-        nbytes = N.call("ebsdvae_wgrad_reduce_batch_work", ctypes.addressof(descs), len(chunk))
-        work = torch.empty(nbytes // 8, dtype=torch.float64, device=chunk[0][0].device)
-        N.call("ebsdvae_wgrad_reduce_batch", ctypes.addressof(descs), len(chunk), work.data_ptr(),
-               N.stream())
+    if not q:
+        return
+    dev = q[0][0].device
+    side = side_stream(dev) if _side_pending(dev) else None
+    if side is not None:
+        # behind the weight gradients on the side stream; partials made on the current
+        # stream (the fused network-end passes) are ordered by the fork
+        _side_use(dev, *[t for e in q for t in e[:2]])
+        ctx = torch.cuda.stream(side)
+    else:
+        ctx = contextlib.nullcontext()
+    with ctx:
+        for i in range(0, len(q), N.MAX_WGRAD_BATCH):
+            chunk = q[i:i + N.MAX_WGRAD_BATCH]
+            descs = (N.WgradReduceDesc * len(chunk))(*[
+                N.WgradReduceDesc(N.ptr(wp), N.ptr(bp), N.ptr(dw), N.ptr(db), S_, cin, cout, kind)
+                for wp, bp, S_, cin, cout, kind, dw, db in chunk])
+            nbytes = N.call("ebsdvae_wgrad_reduce_batch_work", ctypes.addressof(descs), len(chunk))
+            work = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
+            N.call("ebsdvae_wgrad_reduce_batch", ctypes.addressof(descs), len(chunk),
+                   work.data_ptr(), N.stream())
+            if side is not None:
+                _KEEP[_dev_key(dev)].append(work)
+    if side is not None and not _DEFER:
+        _join_side(dev)
 
 
 def _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db):
-    main = torch.cuda.current_stream(wpart.device)
-    for t in (wpart, bpart):   # partials written on the side stream, read on this one
-        t.record_stream(main)
+    e = (wpart, bpart, S_, cin, cout, kind, dw, db)
     if _RQ is not None:
-        _RQ.append((wpart, bpart, S_, cin, cout, kind, dw, db))
-        return
-    _join_side(wpart.device)
-    nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
-    work = torch.empty(nbytes // 8, dtype=torch.float64, device=wpart.device)
-    N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db), cin, cout,
-           kind, work.data_ptr(), N.stream())
+        _RQ.append(e)
+    elif _side_pending(wpart.device):
+        _flush_reduces([e])   # on the side stream that wrote the partials, then joined
+    else:
+        nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
+        work = torch.empty(nbytes // 8, dtype=torch.float64, device=wpart.device)
+        N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db), cin,
+               cout, kind, work.data_ptr(), N.stream())
 
 
 def in_backward_final(g1, w14, y, st, dw14, db14):
@@ -610,13 +687,11 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
     side = _side_stream(gy.device)
     if side is None:
         return _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized)
-    side.wait_stream(torch.cuda.current_stream(gy.device))
-    for t in (src, src_stats, gy, getattr(gy, "ev_gmax", None)):
-        if t is not None:
-            t.record_stream(side)
+    side = _side_use(gy.device, src, src_stats, gy, getattr(gy, "ev_gmax", None))
     with torch.cuda.stream(side):
         wpart, bpart, S_ = _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db,
                                        normalized, reduce=False)
+    _KEEP[_dev_key(gy.device)].extend((wpart, bpart))
     _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
 
 

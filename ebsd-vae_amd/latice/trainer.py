@@ -128,10 +128,20 @@ class VAETrainer:
         (loss, kl, rec), _ = E.loss_forward(x_hat, x, z, mu, std, self.kl_lambda)
         g_xhat, g_z, g_mu, g_std, _ = E.loss_backward(x_hat, x, z, mu, std, self.kl_lambda,
                                                       g_loss=self.one, scale=1.0 / self.world)
-        _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
-        g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P, grads=G)
-        self.reducer.start(0)
-        E.encoder_backward(plan, g_enc, x, se, P, grads=G, packs=packs)
+        # the weight-gradient side stream is joined once, after the encoder backward: the
+        # decoder's slice reductions finish on it while the encoder backward runs
+        with E.deferred_side_join(x.device):
+            _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
+            g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P,
+                                        grads=G)
+            if self.world > 1:
+                # bucket 0 (decoder + heads) is complete on the side stream once it has
+                # caught up with the heads backward: the all-reduce is ordered behind it
+                side = E.side_stream(x.device)
+                E.stream_wait(side, torch.cuda.current_stream(x.device))
+                with torch.cuda.stream(side):
+                    self.reducer.start(0)
+            E.encoder_backward(plan, g_enc, x, se, P, grads=G, packs=packs)
         self.reducer.start(1)
         self.reducer.finish()
         return loss, kl, rec
@@ -155,6 +165,7 @@ class VAETrainer:
         of graphs).  Warm-up steps run first on a side stream, as torch requires."""
         if self.world != 1:
             raise RuntimeError("graph capture is for single-process runs")
+        E.side_stream(x.device)   # the weight-gradient stream exists before the capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

@@ -38,6 +38,12 @@ typedef void* ebsdvae_stream_t; /* hipStream_t */
 const char* ebsdvae_last_error(void);
 int ebsdvae_version(void);
 
+/* ---- stream ordering ------------------------------------------------------------------
+ * `waiter` waits for the work enqueued on `signaler` so far (an event with a device-scope
+ * release: cheaper than the default system-scope fence of torch's Stream.wait_stream).
+ * Used for the weight-gradient side stream's fork / join (latice/engine.py); capturable. */
+int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler);
+
 /* ---- weights ------------------------------------------------------------------------
  * Pack a Conv2d (kind 0: (cout,cin,3,3), latice/model.py:95,148) or ConvTranspose2d
  * (kind 1: (cin,cout,3,3), latice/model.py:102-104) weight into the kernel layout

@@ -1,4 +1,8 @@
-"""A/B of eager step() vs hipGraph replay of the whole training step (N = 1)."""
+"""A/B of eager step() vs hipGraph replay of the whole training step (N = 1), and a bitwise
+check that a replayed step computes the eager step's gradients.
+
+    python tools/graph_ab.py            (EBSDVAE_GRAPH_SIDE=0: capture on one stream)
+"""
 import os
 import sys
 import time
@@ -33,7 +37,18 @@ tr.capture(x)
 g = timeit(tr.replay, 20)
 e2 = timeit(lambda: tr.step(x), 20)
 g2 = timeit(tr.replay, 20)
-print(f"eager {e:.3f} / {e2:.3f} ms   graph {g:.3f} / {g2:.3f} ms")
+print(f"side-in-graph={os.environ.get('EBSDVAE_GRAPH_SIDE', '1')}  eager {e:.3f} / {e2:.3f} ms   "
+      f"graph {g:.3f} / {g2:.3f} ms")
+# the same parameters, eps counter and Adam state: eager forward_backward vs a replay
+state = [t.clone() for t in (tr.flat, tr.exp_avg, tr.exp_avg_sq, tr.step_count, tr.noise_counter)]
+tr.forward_backward(x)
+ge = tr.gflat.clone()
+for t, s in zip((tr.flat, tr.exp_avg, tr.exp_avg_sq, tr.step_count, tr.noise_counter), state):
+    t.copy_(s)
+tr.replay()
+torch.cuda.synchronize()
+diff = (tr.gflat - ge).abs().max().item()
+print(f"replayed vs eager gradients: max |diff| {diff:.3e} ({'bitwise equal' if diff == 0 else 'DIFFER'})")
 # CPU-side enqueue time of one eager step (no synchronisation inside the measured loop)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
