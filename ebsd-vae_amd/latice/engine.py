@@ -599,8 +599,11 @@ def _flush_reduces(q):
     side = side_stream(dev) if _side_pending(dev) else None
     if side is not None:
         # behind the weight gradients on the side stream; partials made on the current
-        # stream (the fused network-end passes) are ordered by the fork
-        _side_use(dev, *[t for e in q for t in e[:2]])
+        # stream (the fused network-end passes) are ordered by a fork -- only then, so a
+        # batch of side-stream partials does not wait for the current stream
+        mine = [t for e in q if not e[8] for t in e[:2]]
+        if mine:
+            _side_use(dev, *mine)
         ctx = torch.cuda.stream(side)
     else:
         ctx = contextlib.nullcontext()
@@ -609,7 +612,7 @@ def _flush_reduces(q):
             chunk = q[i:i + N.MAX_WGRAD_BATCH]
             descs = (N.WgradReduceDesc * len(chunk))(*[
                 N.WgradReduceDesc(N.ptr(wp), N.ptr(bp), N.ptr(dw), N.ptr(db), S_, cin, cout, kind)
-                for wp, bp, S_, cin, cout, kind, dw, db in chunk])
+                for wp, bp, S_, cin, cout, kind, dw, db, _ in chunk])
             nbytes = N.call("ebsdvae_wgrad_reduce_batch_work", ctypes.addressof(descs), len(chunk))
             work = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
             N.call("ebsdvae_wgrad_reduce_batch", ctypes.addressof(descs), len(chunk),
@@ -620,12 +623,13 @@ def _flush_reduces(q):
         _join_side(dev)
 
 
-def _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db):
-    e = (wpart, bpart, S_, cin, cout, kind, dw, db)
+def _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db, on_side=False):
+    """on_side: the partials were written on the side stream (conv_wgrad)."""
+    e = (wpart, bpart, S_, cin, cout, kind, dw, db, on_side)
     if _RQ is not None:
         _RQ.append(e)
     elif _side_pending(wpart.device):
-        _flush_reduces([e])   # on the side stream that wrote the partials, then joined
+        _flush_reduces([e])   # on the side stream, then joined
     else:
         nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
         work = torch.empty(nbytes // 8, dtype=torch.float64, device=wpart.device)
@@ -692,7 +696,7 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
         wpart, bpart, S_ = _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db,
                                        normalized, reduce=False)
     _KEEP[_dev_key(gy.device)].extend((wpart, bpart))
-    _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
+    _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db, on_side=True)
 
 
 def _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized=None,
