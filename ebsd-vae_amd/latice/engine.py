@@ -745,13 +745,23 @@ def _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalize
     _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db)
 
 
-def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
+def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False, ypool=None):
     """Input gradient of `layer`.  prev = (y_prev, st_prev, pmode_prev) of the block feeding
     it: the previous block's InstanceNorm-backward reduce is then fused into the epilogue and
     (gin, part) is returned for in_backward(..., part=part).
     sum_up (pmode_prev == P_UP): where the split kernel supports it, gin is returned already
-    2x2-summed, i.e. at the previous block's resolution (then in_backward takes it as P_ID)."""
+    2x2-summed, i.e. at the previous block's resolution (then in_backward takes it as P_ID).
+    ypool (pmode_prev == P_POOL): the previous block's max-pooled raw output, which its forward
+    conv emitted (FP_POOLOUT).  Only the window maximum receives gradient, and the pool adjoint
+    leaves the reduce sums  sum g*lrelu'(xhat), sum g*lrelu'(xhat)*xhat  unchanged when xhat is
+    taken at the maximum: xhat(max y) = (ypool - mean) * rstd, as IN's scale is positive.  So the
+    reduce reads ypool in identity mode -- a quarter of the bytes of the 2x2 windows of y_prev
+    and no argmax -- while the apply (in_backward) still routes through y_prev's windows."""
     B, H, W, _ = gy.shape
+    hw_prev = None if prev is None else prev[0].shape[1] * prev[0].shape[2]
+    if prev is not None and prev[2] == P_POOL and ypool is not None and \
+            os.environ.get("EBSDVAE_POOL_REDUCE", "1") != "0":
+        prev = (ypool, prev[1], P_ID)
     if wd is None:
         wd = pack_weight(w, layer, dgrad=True, scaled=getattr(gy, "ev_gmax", None) is not None)
     if (sum_up and prev is not None and prev[2] == P_UP and wd.pieces
@@ -783,7 +793,7 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False):
         bst = _empty(B, layer.cin, 2, like=gy)
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_f16_bst", N.ptr(gy),
                 N.ptr(gmax), gmax.shape[1], N.ptr(wd.t), N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev),
-                pmode, part.data_ptr(), N.ptr(bst), y_prev.shape[1] * y_prev.shape[2], B, H, W,
+                pmode, part.data_ptr(), N.ptr(bst), hw_prev, B, H, W,
                 layer.cout, layer.cin, N.stream(), tag=tag + " +inbwd", pieces=wd.pieces, nbytes=nbd)
         part.ev_bst = bst
         return gin, part
@@ -906,7 +916,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
         if i > 0:
             P = plan.enc[i - 1]
             g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode),
-                                      wd=_wp(packs, L.name, 1))
+                                      wd=_wp(packs, L.name, 1), ypool=saved.get(L.name + ".pool_in"))
         elif need_gx:
             B, H, W, _ = gy.shape
             gx = _empty(B, 1, H, W, like=gy)

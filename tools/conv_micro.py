@@ -37,6 +37,12 @@ CASES = {
     "dgrad32": ("dgrad", 128, 32, 32, P_ID),
     "dgrad64": ("dgrad", 64, 64, 64, P_ID),
     "dgrad32u": ("dgrad", 128, 32, 32, P_UP),
+    # the encoder's pool-fed layers' input gradients, fused reduce over the 2x2 windows of
+    # the producer's y (P_POOL) or over its pooled raw output (P_ID, engine ypool)
+    "dgrad32to64p": ("dgrad", 64, 32, 64, P_POOL),
+    "dgrad32to64i": ("dgrad", 64, 32, 64, P_ID),
+    "dgrad64to128p": ("dgrad", 32, 64, 128, P_POOL),
+    "dgrad64to128i": ("dgrad", 32, 64, 128, P_ID),
     "dgrad128": ("dgrad", 32, 128, 128, P_ID),
     "wgrad32": ("wgrad", 128, 32, 32, ACT_NORM),
     "wgrad32u": ("wgrad", 128, 32, 32, ACT_NORM_UP),
