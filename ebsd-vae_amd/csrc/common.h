@@ -45,6 +45,17 @@ EV_DEVINL float2 norm_fs(float2 st) { return make_float2(st.y, -st.x * st.y); }
 EV_DEVINL float normact_fs(float v, float2 fs) { return lrelu(fmaf(v, fs.x, fs.y)); }
 
 EV_DEVINL float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// The first conv (1 -> C, latice/model.py:110) at one pixel and one output channel: nb[t] =
+// x[h + t/3 - 1][w + t%3 - 1] (0 outside the image), wt = the channel's 9 taps.  One fixed fma
+// chain, shared by the forward (conv_first_fwd_kernel) and the first block's backward, which
+// recomputes y0 from x with it instead of re-reading y0 (bit-identical by construction).
+EV_DEVINL float first_conv_px(const float (&nb)[9], const float (&wt)[9], float bias) {
+  float s = nb[0] * wt[0];
+#pragma unroll
+  for (int t = 1; t < 9; ++t) s = fmaf(nb[t], wt[t], s);
+  return s + bias;
+}
 EV_DEVINL void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 EV_DEVINL float4 max4(float4 a, float4 b) {

@@ -225,9 +225,118 @@ __global__ __launch_bounds__(256) void conv_cout1_dgrad_kernel(
   }
 }
 
+// ------------------------------------------------------------------ first conv (cin == 1)
+// y0 = conv3x3(x, w0) + b0 for C == 32 output channels on the VALU (first_conv_px, the fma
+// chain the first block's backward recomputes y0 with), plus its InstanceNorm partials
+// {mean, M2} per row band of FIRST_PX pixels.  It is a write-bound kernel (1 input channel,
+// 32 output channels: 128 B written per 4 B read); block = one row band of one image, x band
+// + halo staged in LDS, 8 threads per pixel (4 channels each: one 16-B store, a pixel's 128 B
+// contiguous), the band's values kept in registers for the two-pass statistics.
+constexpr int FIRST_C = 32, FIRST_PX = 512, FIRST_NPT = FIRST_PX / 32;
+
+static int first_rows(int W) { return (W > 0 && W < FIRST_PX && FIRST_PX % W == 0) ? FIRST_PX / W : 0; }
+
+__global__ __launch_bounds__(256) void conv_first_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ w0, const float* __restrict__ b0,
+    float* __restrict__ y, float2* __restrict__ part, int H, int W, int TH) {
+  extern __shared__ float xs[];   // (TH + 2) x (W + 2)
+  __shared__ float red[8][32][4];
+  const int tile = blockIdx.x, b = blockIdx.y, T = gridDim.x;
+  const int tid = threadIdx.x, cg = tid & 7, pr = tid >> 3;
+  const int c = cg * 4, r0 = tile * TH, WP = W + 2;
+  const float* xb = x + (size_t)b * H * W;
+  for (int i = tid; i < (TH + 2) * WP; i += 256) {
+    const int r = i / WP, cc = i - r * WP;
+    const int gh = r0 - 1 + r, gw = cc - 1;
+    xs[i] = (gh >= 0 && gh < H && gw >= 0 && gw < W) ? xb[gh * W + gw] : 0.f;
+  }
+  float wt[4][9], bb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[k][t] = w0[(c + k) * 9 + t];
+    bb[k] = b0 ? b0[c + k] : 0.f;
+  }
+  __syncthreads();
+  float v[FIRST_NPT][4];
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  float* yb = y + ((size_t)b * H * W + (size_t)r0 * W) * FIRST_C + c;
+#pragma unroll
+  for (int j = 0; j < FIRST_NPT; ++j) {
+    const int p = pr + 32 * j, h = p / W, w = p - h * W;
+    float nb[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) nb[t] = xs[(h + t / 3) * WP + w + t % 3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[j][k] = first_conv_px(nb, wt[k], bb[k]);
+      s[k] += v[j][k];
+    }
+#ifdef EV_FIRST_NT   // experiment: streaming (non-temporal) stores
+    float* o = yb + (size_t)p * FIRST_C;
+    __builtin_nontemporal_store(v[j][0], o);
+    __builtin_nontemporal_store(v[j][1], o + 1);
+    __builtin_nontemporal_store(v[j][2], o + 2);
+    __builtin_nontemporal_store(v[j][3], o + 3);
+#else
+    st4(yb + (size_t)p * FIRST_C, make_float4(v[j][0], v[j][1], v[j][2], v[j][3]));
+#endif
+  }
+  // band statistics per channel, fixed order: 32 pixel lanes folded through LDS
+  float mean[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[cg][pr][k] = s[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float a = 0.f;
+    for (int i = 0; i < 32; ++i) a += red[cg][i][k];
+    mean[k] = a * (1.0f / FIRST_PX);
+  }
+  float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < FIRST_NPT; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = v[j][k] - mean[k];
+      q[k] = fmaf(d, d, q[k]);
+    }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[cg][pr][k] = q[k];
+  __syncthreads();
+  if (pr == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float a = 0.f;
+      for (int i = 0; i < 32; ++i) a += red[cg][i][k];
+      part[((size_t)b * T + tile) * FIRST_C + c + k] = make_float2(mean[k], a);
+    }
+  }
+}
+
 }  // namespace ev
 
 using namespace ev;
+
+extern "C" int ebsdvae_conv_first_stat_tiles(int H, int W) {
+  const int th = first_rows(W);
+  return (th > 0 && H % th == 0) ? H / th : -1;
+}
+
+extern "C" int ebsdvae_conv_first_fwd(const float* x, const float* w0, const float* b0, float* y,
+                                      float* part, int B, int H, int W, int C,
+                                      ebsdvae_stream_t stream) {
+  EV_REQUIRE(x && w0 && y && part && B > 0 && C == FIRST_C,
+             "conv_first_fwd: bad args (C must be %d)", FIRST_C);
+  const int th = first_rows(W);
+  EV_REQUIRE(th > 0 && FIRST_PX % W == 0 && H % th == 0,
+             "conv_first_fwd: %dx%d unsupported (W must divide %d)", H, W, FIRST_PX);
+  hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(H / th, B), dim3(256),
+                     (size_t)(th + 2) * (W + 2) * sizeof(float), (hipStream_t)stream, x, w0, b0, y,
+                     (float2*)part, H, W, th);
+  return evh::check_launch("conv_first_fwd");
+}
 
 extern "C" int ebsdvae_conv3x3_cout1_fwd(const float* src, const float* src_stats, int src_mode,
                                          const float* w, const float* bias, float* out, int flip,

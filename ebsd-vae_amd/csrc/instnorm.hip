@@ -234,7 +234,9 @@ __global__ __launch_bounds__(256) void in_bwd_finalize_kernel(const double2* __r
 // written (the input x needs no gradient).
 // Partials are per (b, tile) "slice" in the [slice][tap][co][ci] layout of
 // ebsdvae_wgrad_reduce.
-enum EdgeFuse : int { FUSE_FINAL = 1, FUSE_FIRST = 2 };
+// FUSE_FIRST_RC: FUSE_FIRST with y0 recomputed from the staged x band (first_conv_px, the
+// forward's fma chain: conv_first_fwd_kernel) instead of read -- 512 MB less per step at B=256
+enum EdgeFuse : int { FUSE_FINAL = 1, FUSE_FIRST = 2, FUSE_FIRST_RC = 3 };
 constexpr int EDGE_NB_ITEMS = 8;   // staged neighbour-source items per thread (<= 2048 per band)
 
 EV_DEVINL void wave_fold8(float& v) {  // sum over the 8 pixel rows of a wave (lanes l, l^8, ...)
@@ -248,8 +250,11 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     const float* __restrict__ gsrc, const float* __restrict__ w14, const float* __restrict__ y,
     const float2* __restrict__ st, const float2* __restrict__ bst, const float* __restrict__ x,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart,
-    float* __restrict__ gy, int H, int W, int T, float* __restrict__ gmax) {
+    float* __restrict__ gy, int H, int W, int T, float* __restrict__ gmax,
+    const float* __restrict__ b0 = nullptr) {
   constexpr int C = 32, CG = 8, NPR = 32;
+  constexpr bool RC = FUSE == FUSE_FIRST_RC;
+  constexpr int FUSE_ = RC ? FUSE_FIRST : FUSE;   // RC is FIRST with y recomputed
   float amax = 0.f;   // FINAL apply: max |gy| of this thread (gmax: per-tile maxima, f16 convs)
   __shared__ double red[2][4][256];
   __shared__ float wred[4][CG][37];
@@ -267,12 +272,14 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) { m1[k] = bp[k].x; m2[k] = bp[k].y; }
   }
-  float wv[4][9];
-  if (FUSE == FUSE_FINAL) {
+  float wv[4][9], bb0[4];   // FINAL: w14 (1, 32, 3, 3); RC: w0 (32, 1, 3, 3) and b0
+  if (FUSE_ == FUSE_FINAL || RC) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 4; ++k) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) wv[k][t] = w14[(c + k) * 9 + t];
+      bb0[k] = (RC && b0) ? b0[c + k] : 0.f;
+    }
   }
   double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
   float wacc[4][9];
@@ -284,7 +291,7 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
   const float* yb = y + (size_t)b * H * W * C;
   // the 1-channel neighbour source (FINAL: g1, FIRST: x) of this row band plus its 1-pixel
   // halo, staged once in LDS with coalesced loads (zero padding at the image border)
-  const float* src1 = ((FUSE == FUSE_FINAL) ? gsrc : x) + (size_t)b * H * W;
+  const float* src1 = ((FUSE_ == FUSE_FINAL) ? gsrc : x) + (size_t)b * H * W;
   extern __shared__ float nbs[];   // (rows + 2) x (W + 2)
   const int r0 = tile * rows, WP = W + 2;
   {
@@ -308,11 +315,11 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
   // gnext) loads are issued before this group is processed
   // the FINAL reduce is VALU-heavy (9-tap recompute + 36 weight-gradient FMAs per pixel)
   // and register-bound: 2 pixels per group, loaded at the group's start, no prefetch
-  constexpr bool PF = !(FUSE == FUSE_FINAL && !APPLY);
+  constexpr bool PF = !(FUSE_ == FUSE_FINAL && !APPLY);
   constexpr int U = PF ? 4 : 2;
-  constexpr bool LG = FUSE == FUSE_FIRST;
+  constexpr bool LG = FUSE_ == FUSE_FIRST;
   auto ldy = [&](int p) {
-    return p < p1 ? ld4(yb + (size_t)p * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    return (!RC && p < p1) ? ld4(yb + (size_t)p * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   auto ldg = [&](int p) {
     return (LG && p < p1) ? ld4(gsrc + ((size_t)b * H * W + p) * C + c)
@@ -347,12 +354,12 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int kh = t / 3, kw = t % 3;
-      const int lr = (FUSE == FUSE_FINAL) ? h - r0 + 2 - kh : h - r0 + kh;
-      const int lc = (FUSE == FUSE_FINAL) ? w + 2 - kw : w + kw;
+      const int lr = (FUSE_ == FUSE_FINAL) ? h - r0 + 2 - kh : h - r0 + kh;
+      const int lc = (FUSE_ == FUSE_FINAL) ? w + 2 - kw : w + kw;
       nb[t] = nbs[lr * WP + lc];
     }
     float ga[4];
-    if (FUSE == FUSE_FINAL) {
+    if (FUSE_ == FUSE_FINAL) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float s = 0.f;
@@ -366,7 +373,11 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       ga[0] = g4.x; ga[1] = g4.y; ga[2] = g4.z; ga[3] = g4.w;
     }
     const float4 y4 = ycur[u];
-    const float yy[4] = {y4.x, y4.y, y4.z, y4.w};
+    float yy[4] = {y4.x, y4.y, y4.z, y4.w};
+    if (RC) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) yy[k] = first_conv_px(nb, wv[k], bb0[k]);
+    }
     float o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -375,21 +386,21 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       if (!APPLY) {
         a1[k] += (double)gx;
         a2[k] = fma((double)gx, (double)xh, a2[k]);
-        if (FUSE == FUSE_FINAL) {
+        if (FUSE_ == FUSE_FINAL) {
           const float av = lrelu(xh);
 #pragma unroll
           for (int t = 0; t < 9; ++t) wacc[k][t] = fmaf(nb[t], av, wacc[k][t]);
         }
       } else {
         o[k] = rstd[k] * (gx - m1[k] - xh * m2[k]);
-        if (FUSE == FUSE_FIRST) {
+        if (FUSE_ == FUSE_FIRST) {
           bacc[k] += o[k];
 #pragma unroll
           for (int t = 0; t < 9; ++t) wacc[k][t] = fmaf(o[k], nb[t], wacc[k][t]);
         }
       }
     }
-    if (APPLY && FUSE == FUSE_FINAL) {
+    if (APPLY && FUSE_ == FUSE_FINAL) {
       st4(gy + ((size_t)b * H * W + p) * C + c, make_float4(o[0], o[1], o[2], o[3]));
       amax = fmaxf(fmaxf(amax, fmaxf(fabsf(o[0]), fabsf(o[1]))), fmaxf(fabsf(o[2]), fabsf(o[3])));
     }
@@ -400,7 +411,7 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     }
   }
   const int slice = b * T + tile;
-  if (FUSE == FUSE_FINAL && APPLY && gmax) {   // block-uniform: one maximum per (image, tile)
+  if (FUSE_ == FUSE_FINAL && APPLY && gmax) {   // block-uniform: one maximum per (image, tile)
     __shared__ float wmax[4];
     for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
     if (lane == 0) wmax[wave] = amax;
@@ -424,7 +435,7 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       for (int k = 0; k < 4; ++k) op[k] = make_double2(u[k], v[k]);
     }
   }
-  if ((FUSE == FUSE_FINAL && !APPLY) || (FUSE == FUSE_FIRST && APPLY)) {
+  if ((FUSE_ == FUSE_FINAL && !APPLY) || (FUSE_ == FUSE_FIRST && APPLY)) {
     // fold the 36 weight partials (+ bias) of the block: in-wave over its 8 pixel rows,
     // then across the 4 waves in order
 #pragma unroll
@@ -439,8 +450,8 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       wave_fold8(v);
       // bias: FINAL keeps one scalar (k == 0, cg == 0 lane); FIRST keeps 4 per channel group
       if (lane < CG) {
-        if (FUSE == FUSE_FINAL && k == 0) wred[wave][lane][36] = v;
-        if (FUSE == FUSE_FIRST) bacc[k] = v;
+        if (FUSE_ == FUSE_FINAL && k == 0) wred[wave][lane][36] = v;
+        if (FUSE_ == FUSE_FIRST) bacc[k] = v;
       }
     }
     __syncthreads();
@@ -452,9 +463,9 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       const int k = e / 9, t = e % 9;
       wpart[((size_t)slice * 9 + t) * 32 + g * 4 + k] = s;
     }
-    if (FUSE == FUSE_FINAL && tid == 0)
+    if (FUSE_ == FUSE_FINAL && tid == 0)
       bpart[slice] = wred[0][0][36] + wred[1][0][36] + wred[2][0][36] + wred[3][0][36];
-    if (FUSE == FUSE_FIRST) {
+    if (FUSE_ == FUSE_FIRST) {
       __syncthreads();
       if (lane < CG) {
 #pragma unroll
@@ -618,6 +629,22 @@ extern "C" int ebsdvae_in_bwd_final_apply_max(const float* g1, const float* w14,
                      (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
                      H, W, T, gmax);
   return evh::check_launch("in_bwd_final_apply_max");
+}
+
+extern "C" int ebsdvae_in_bwd_first_apply_wgrad_rc(const float* gnext, const float* w0,
+                                                   const float* b0, const float* stats,
+                                                   const float* bstats, const float* x, float* wpart,
+                                                   float* bpart, int B, int H, int W, int C,
+                                                   ebsdvae_stream_t stream) {
+  EV_REQUIRE(gnext && w0 && stats && bstats && x && wpart && bpart && C == 32,
+             "in_bwd_first_apply_wgrad_rc: bad args (C must be 32)");
+  const int T = in_bwd_tiles_host(H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST_RC, true>), dim3(T, B), dim3(256),
+                     edge_lds(H, W, T), (hipStream_t)stream, gnext, w0, (const float*)nullptr,
+                     (const float2*)stats, (const float2*)bstats, x, (double2*)nullptr, wpart, bpart,
+                     (float*)nullptr, H, W, T, (float*)nullptr, b0);
+  return evh::check_launch("in_bwd_first_apply_wgrad_rc");
 }
 
 extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float* y,

@@ -26,6 +26,9 @@ SIGNATURES = {
     "ebsdvae_last_error": [],
     "ebsdvae_version": [],
     "ebsdvae_stream_wait": [P, P],
+    "ebsdvae_conv_first_stat_tiles": [I, I],
+    "ebsdvae_conv_first_fwd": [P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_first_apply_wgrad_rc": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_pack_conv_weight": [P, P, I, I, I, I, P],
     "ebsdvae_pack_conv_weights": [P, I, P],
     "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, P, I, I, I, I, I, P],
@@ -91,7 +94,7 @@ _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": 
             "ebsdvae_cosine_topk_work": ctypes.c_size_t,
             "ebsdvae_heads_wgrad_work": ctypes.c_size_t, "ebsdvae_pack_split_bytes": ctypes.c_size_t}
 # queries that return a value rather than a status
-QUERIES = {"ebsdvae_version", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
+QUERIES = {"ebsdvae_version", "ebsdvae_conv_first_stat_tiles", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
            "ebsdvae_wgrad_reduce_batch_work", "ebsdvae_cosine_topk_work",
            "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_in_bwd_final_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",

@@ -380,6 +380,28 @@ def pool_out_ok(layer: ConvLayer, wp) -> bool:
         "ebsdvae_conv3x3_split_pool_ok", layer.H, layer.H, layer.cin, layer.cout, wp.pieces))
 
 
+# The first conv (cin = 1) runs on the VALU with a fixed fma chain (ebsdvae_conv_first_fwd), so
+# the first block's backward can recompute y0 from x bit-identically instead of re-reading it
+# (ebsdvae_in_bwd_first_apply_wgrad_rc).  EBSDVAE_FIRST_VALU=0: the fp32-MFMA conv + re-read.
+_FIRST_VALU = os.environ.get("EBSDVAE_FIRST_VALU", "1") != "0"
+
+
+def _conv_first(x, layer: ConvLayer, w, b, B):
+    H = layer.H
+    T = N.call("ebsdvae_conv_first_stat_tiles", H, H)
+    y = _empty(B, H, H, layer.cout, like=w)
+    part = _empty(B, T, layer.cout, 2, like=w)
+    st = _empty(B, layer.cout, 2, like=w)
+    tag = f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m{layer.src_mode} valu"
+    _launch("conv3x3_fwd", conv_flops(B, H, H, 1, layer.cout), N.call, "ebsdvae_conv_first_fwd",
+            N.ptr(x), N.ptr(w), N.ptr(b), N.ptr(y), N.ptr(part), B, H, H, layer.cout, N.stream(),
+            tag=tag, nbytes=4 * (x.numel() + y.numel()))
+    N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
+           N.stream())
+    y.ev_first_valu = True   # in_backward_first may recompute it from x
+    return y, st
+
+
 def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=None, mode=None,
                  pool_out=False):
     """One conv block forward: y (B,H,H,cout) pre-norm + IN stats {mean,rstd} (B,cout,2).
@@ -390,6 +412,9 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     producer side of that (ebsdvae_conv3x3_fwd_split_pooled)."""
     H = layer.H
     src_mode = layer.src_mode if mode is None else mode
+    if (layer.cin == 1 and layer.cout == 32 and src_mode == ACT_RAW and not keep_act
+            and not pool_out and _FIRST_VALU and N.call("ebsdvae_conv_first_stat_tiles", H, H) > 0):
+        return _conv_first(src, layer, w, b, B)
     if wp is None:
         wp = pack_weight(w, layer, dgrad=False)
     y = _empty(B, H, H, layer.cout, like=w)
@@ -663,10 +688,12 @@ def in_backward_final(g1, w14, y, st, dw14, db14):
     return gy
 
 
-def in_backward_first(gnext, y, st, x, dw0, db0, part=None):
+def in_backward_first(gnext, y, st, x, dw0, db0, part=None, w0=None, b0=None):
     """Backward of the first conv block (latice/model.py:110): writes dW/db of the 1->32
     conv directly from the InstanceNorm-backward apply pass (gy is never materialised).
-    part: reduce-pass sums from the fused input-gradient conv (None: reduce here)."""
+    part: reduce-pass sums from the fused input-gradient conv (None: reduce here).
+    w0, b0: the first conv's parameters; with them, and y from ebsdvae_conv_first_fwd, y is
+    recomputed from x instead of read."""
     B, H, W, C = y.shape
     if part is None:
         T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
@@ -678,8 +705,12 @@ def in_backward_first(gnext, y, st, x, dw0, db0, part=None):
     S_ = B * T
     wpart = _empty(S_, 9, C, 1, like=y)
     bpart = _empty(S_, C, like=y)
-    N.call("ebsdvae_in_bwd_first_apply_wgrad", N.ptr(gnext), N.ptr(y), N.ptr(st), N.ptr(bst),
-           N.ptr(x), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
+    if w0 is not None and getattr(y, "ev_first_valu", False):
+        N.call("ebsdvae_in_bwd_first_apply_wgrad_rc", N.ptr(gnext), N.ptr(w0), N.ptr(b0), N.ptr(st),
+               N.ptr(bst), N.ptr(x), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
+    else:
+        N.call("ebsdvae_in_bwd_first_apply_wgrad", N.ptr(gnext), N.ptr(y), N.ptr(st), N.ptr(bst),
+               N.ptr(x), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
     _reduce_slices(wpart, bpart, S_, 1, C, KIND_CONV, dw0, db0)
 
 
@@ -894,7 +925,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
             wn, bn = L.name + ".weight", L.name + ".bias"
             dw = _grad_buf(grads, wn, params[wn])
             db = _grad_buf(grads, bn, params[bn])
-            in_backward_first(g_next, y, st, x, dw, db, part=part)
+            in_backward_first(g_next, y, st, x, dw, db, part=part, w0=params[wn], b0=params[bn])
             out[wn], out[bn] = dw, db
             break
         gy = in_backward(g_next, L.pmode, y, st, part=part)

@@ -96,6 +96,15 @@ int ebsdvae_conv3x3_dgrad_inbwd(const float* g, const float* wpack, float* gin,
  * out[b,h,w] = bias + sum act(src)*w[ci][tap'] with tap' = flip ? 8-tap : tap.
  * w is (1,cin,3,3) contiguous (== (cin,1,3,3)).  With flip=1, RAW source and
  * w = encoder.0 weight it is the input gradient of the first conv. bias may be NULL. */
+/* The first conv nn.Conv2d(1, C, 3, 1, 1) (latice/model.py:110), C == 32, on the VALU:
+ * y (B,H,W,C) NHWC = conv(x (B,1,H,W), w0 (C,1,3,3)) + b0 (b0 may be NULL), and its
+ * InstanceNorm partials part[b][t][c] = {mean, M2} over row band t of n = H*W/T pixels,
+ * T = ebsdvae_conv_first_stat_tiles(H, W) (-1: shape unsupported; W must divide 512), for
+ * ebsdvae_in_stats_finalize.  Its arithmetic is the fixed fma chain that
+ * ebsdvae_in_bwd_first_apply_wgrad_rc recomputes y with. */
+int ebsdvae_conv_first_stat_tiles(int H, int W);
+int ebsdvae_conv_first_fwd(const float* x, const float* w0, const float* b0, float* y,
+                           float* part, int B, int H, int W, int C, ebsdvae_stream_t stream);
 int ebsdvae_conv3x3_cout1_fwd(const float* src, const float* src_stats, int src_mode,
                               const float* w, const float* bias, float* out, int flip,
                               int B, int H, int W, int cin, ebsdvae_stream_t stream);
@@ -287,6 +296,13 @@ int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float* y, const f
                                      const float* bstats, const float* x, float* wpart,
                                      float* bpart, int B, int H, int W, int C,
                                      ebsdvae_stream_t stream);
+/* As ebsdvae_in_bwd_first_apply_wgrad, with the first conv's output y0 recomputed from x, w0
+ * (encoder.0 weight, (C,1,3,3)) and b0 (encoder.0 bias) instead of read: bit-identical to the
+ * y0 that ebsdvae_conv_first_fwd wrote (one shared fma chain), 4*B*H*W*C bytes less traffic. */
+int ebsdvae_in_bwd_first_apply_wgrad_rc(const float* gnext, const float* w0, const float* b0,
+                                        const float* stats, const float* bstats, const float* x,
+                                        float* wpart, float* bpart, int B, int H, int W, int C,
+                                        ebsdvae_stream_t stream);
 /* gradient of nearest x2 upsampling: out[b,h,w,c] = sum of the 2x2 block of g (at 2H) */
 int ebsdvae_upsample2_bwd(const float* g, float* out, int B, int H, int W, int C,
                           ebsdvae_stream_t stream);

@@ -388,6 +388,44 @@ def test_fused_first_conv_weight_grad(cuda):
     assert np.abs(host(db) - rb).max() < 1e-4 * max(1.0, np.abs(rb).max())
 
 
+@pytest.mark.parametrize("H", [128, 256, 64])
+def test_first_conv_valu_and_recomputed_backward(cuda, H):
+    """ebsdvae_conv_first_fwd (VALU fma chain) vs the oracle conv + InstanceNorm statistics,
+    and the first block's backward with y0 recomputed from x
+    (ebsdvae_in_bwd_first_apply_wgrad_rc) bit-identical to the one that reads y0."""
+    rng = np.random.default_rng(23 + H)
+    B, C = 2, 32
+    x = np.floor(rng.random((B, 1, H, H)) * 255) / 255
+    w = rng.standard_normal((C, 1, 3, 3)) / 3.0
+    b = rng.standard_normal(C) * 0.1
+    layer = E.ConvLayer("encoder.0.0", E.KIND_CONV, 1, C, H, E.ACT_RAW, E.P_ID)
+    xd, wd, bd = dev(x), dev(w), dev(b)
+    y, st = E.conv_forward(xd, None, layer, wd, bd, B)
+    assert getattr(y, "ev_first_valu", False)
+    ref = O.conv3x3(x.transpose(0, 2, 3, 1), w, b)
+    assert O.rel_err(host(y), ref) < 1e-6
+    xh, rm, rr = O.instance_norm(ref)
+    got = host(st)
+    assert O.rel_err(got[..., 0], rm[:, 0, 0, :]) < 1e-5
+    assert O.rel_err(got[..., 1], rr[:, 0, 0, :]) < 1e-5
+    gn = dev(rng.standard_normal((B, H, H, C)))
+    dw_rc, db_rc = torch.empty(C, 1, 3, 3, device="cuda"), torch.empty(C, device="cuda")
+    dw_rd, db_rd = torch.empty_like(dw_rc), torch.empty_like(db_rc)
+    E.in_backward_first(gn, y, st, xd, dw_rc, db_rc, w0=wd, b0=bd)   # recomputes y0
+    E.in_backward_first(gn, y, st, xd, dw_rd, db_rd)                   # reads y0
+    torch.cuda.synchronize()
+    assert torch.equal(dw_rc, dw_rd) and torch.equal(db_rc, db_rd)
+    gy = O.instance_norm_bwd(host(gn) * O.lrelu_slope(xh), xh, rr)
+    rw, rb = O.conv3x3_wgrad(x.transpose(0, 2, 3, 1), gy)
+    # the fused first-block weight gradient accumulates B*H*W strongly cancelling products in
+    # fp32 (the same kernel reading y0 gives the same bits, asserted above): 5e-4 at 256^2
+    assert O.rel_err(host(dw_rc), rw) < (1e-4 if H <= 128 else 1e-3)
+    # db is analytically zero (a bias before InstanceNorm): fp32 cancellation over the plane,
+    # bounded by a few ulps of the L1 norm of the summands
+    l1 = np.abs(gy).sum(axis=(0, 1, 2))
+    assert (np.abs(host(db_rc) - rb) <= 2e-8 * l1).all()
+
+
 def test_batched_weight_pack_matches_single_packs(cuda):
     """ebsdvae_pack_conv_weights (one launch per step) == per-layer ebsdvae_pack_conv_weight."""
     plan = E.build_plan(32, 16, 128)
