@@ -346,7 +346,7 @@ def main():
                     help="timed steps of the strict fp32-MFMA leg (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
-    ap.add_argument("--probe-every", type=int, default=5,
+    ap.add_argument("--probe-every", type=int, default=10,
                     help="bracket the conv launches with HIP events on every k-th timed step")
     ap.add_argument("--precision", default=None, choices=["fp32", "bf16x6", "bf16x3", "f16x3"],
                     help="conv arithmetic (default: the engine default, f16x3)")
@@ -404,7 +404,7 @@ def main():
             # the stream a few microseconds, so bracketing every launch of every step would
             # slow the step the value is quoted on by ~2 %.  These steps keep the weight
             # gradients on the main stream, so that every launch is timed alone (overlapped
-            # launches would each carry the other's time); ~1.4 % slower, one step in five
+            # launches would each carry the other's time); ~5 % slower, one step in ten
             with probe, E.serial_streams():
                 out = trainer.step(x)
             probed += 1

@@ -272,15 +272,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
       v[j][k] = first_conv_px(nb, wt[k], bb[k]);
       s[k] += v[j][k];
     }
-#ifdef EV_FIRST_NT   // experiment: streaming (non-temporal) stores
-    float* o = yb + (size_t)p * FIRST_C;
-    __builtin_nontemporal_store(v[j][0], o);
-    __builtin_nontemporal_store(v[j][1], o + 1);
-    __builtin_nontemporal_store(v[j][2], o + 2);
-    __builtin_nontemporal_store(v[j][3], o + 3);
-#else
     st4(yb + (size_t)p * FIRST_C, make_float4(v[j][0], v[j][1], v[j][2], v[j][3]));
-#endif
   }
   // band statistics per channel, fixed order: 32 pixel lanes folded through LDS
   float mean[4];

@@ -12,7 +12,7 @@ T=${1:-r02}
 R=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=$R/gpurun_out
-B="python3 $R/bench.py --no-cpu-baseline --c4-batches 0 --c5-steps 0 --strict-fp32-steps 0"
+B="python3 $R/bench.py --probe-every 5 --no-cpu-baseline --c4-batches 0 --c5-steps 0 --strict-fp32-steps 0"
 A="SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_trace -o run -- $B --steps 20 --warmup 5 > $O/${T}_bench_traced.json 2> $O/${T}_trace.log && echo trace ok && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${T}_fetch -o run -- $B --steps 3 --warmup 1 --no-probe > $O/${T}_fetch.log 2>&1 && echo fetch ok && \
