@@ -98,14 +98,28 @@ static bool wg_pipe() {
   }();
   return v;
 }
+// output channels per block of the pipelined kernel: 32 (cout 32), 64, or -- with
+// EBSDVAE_WG_CO128=1 -- 128 (8-wave blocks, one per CU, for cout % 128 == 0).  Alone the wide
+// blocks stage 1.28x fewer elements per FLOP and run 7-8 % faster (128->128 @32 232 -> 215 us,
+// 64->128 @32 116 -> 107 us), but the step got ~0.1 ms slower: a 112-KB block owns its CU, so
+// the weight gradients on the side stream crowd out the input-gradient chain beside them.
+static int wg_pipe_cot(int cout) {
+  static const bool wide = [] {
+    const char* e = getenv("EBSDVAE_WG_CO128");
+    return e && e[0] == '1';
+  }();
+  return cout == 32 ? 32 : ((wide && cout % 128 == 0) ? 128 : 64);
+}
 static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
   if (H % 8 || W % 8 || cin % 32 || !(cout == 32 || cout % 64 == 0)) return false;
   g->TW = 8; g->TH = 8; g->NI = 1;
   g->ntx = W / 8; g->nty = H / 8;
   g->lTW = 3; g->ltpx = 6;
   g->tiles = (int)((long)B * g->ntx * g->nty);
-  const int co_t = cout == 32 ? 1 : cout / 64;
-  const int want = wg_block_target(64) / (co_t * (cin / 32));
+  const int cot = wg_pipe_cot(cout);
+  const int co_t = cout == 32 ? 1 : cout / cot;
+  // 8-wave blocks fill a CU alone: half the block target keeps one wave of blocks
+  const int want = wg_block_target(64) / (cot == 128 ? 2 : 1) / (co_t * (cin / 32));
   int tps = 4;
   while ((g->tiles + tps - 1) / tps > (want > 1 ? want : 1)) tps *= 2;
   g->tps = tps;
@@ -115,7 +129,7 @@ static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
 
 // 1-D grid of wgrad_pipe_kernel: 8 x ceil(slices / 8) x (co tiles x ci tiles) blocks
 static dim3 wg_pipe_grid(const WgGeom& g, int cin, int cout) {
-  const int nm = (cout == 32 ? 1 : cout / 64) * (cin / 32);
+  const int nm = (cout == 32 ? 1 : cout / wg_pipe_cot(cout)) * (cin / 32);
   return dim3(8 * ((g.slices + 7) / 8) * nm);
 }
 
@@ -439,6 +453,7 @@ EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[2][9], const double (&bs)[4], cha
                                   int co0, int ci0, int Cin, int Cout, float gsc, bool do_bias) {
   constexpr int CO_T = NWCO * 32;
   constexpr int QG = CO_T / 4;
+  constexpr int NTH = NWCO * 2 * KSPLIT * 64;   // threads per block
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
   if (KSPLIT == 2) {
@@ -479,12 +494,12 @@ EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[2][9], const double (&bs)[4], cha
   if (do_bias) {
     double* xb = reinterpret_cast<double*>(wsm);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xb[i * 256 + tid] = bs[i];
+    for (int i = 0; i < 4; ++i) xb[i * NTH + tid] = bs[i];
     __syncthreads();
     if (tid < CO_T) {
       const int qq = tid >> 2, i = tid & 3;
       double sum = 0.0;
-      for (int m = qq; m < 256; m += QG) sum += xb[i * 256 + m];
+      for (int m = qq; m < NTH; m += QG) sum += xb[i * NTH + m];
       bpart[(size_t)slice * Cout + co0 + tid] = (float)sum;
     }
   }
@@ -711,8 +726,10 @@ EV_DEVINL void static_for(F&& f) {
 // (a whole tile of MFMA work covers every load).  One barrier per tile.  The serial kernel
 // spends most of its time there: without its staging it runs 2.3-2.7x faster, without its
 // loads 1.3x (tools/micro_variants.sh, EV_WG_NOSTORE / EV_WG_NOLOAD).
+// NWCO = 4 (co 128 x ci 32, 8 waves, one block per CU by LDS): the activation halo of a tile
+// is staged once per 128 output channels instead of once per 64 (EBSDVAE_WG_CO128)
 template <int NP, int NWCO, int KSPLIT, int MODE>
-__global__ __launch_bounds__(256, 2) void wgrad_pipe_kernel(
+__global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgrad_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats,
     const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
     int H, int W, int Cin, int Cout, WgGeom g, const float* __restrict__ gmax, int gmT) {
@@ -723,8 +740,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_pipe_kernel(
   constexpr int CO_T = NWCO * 32;
   constexpr int GSB = CO_T * 2 + 32;       // gy image row stride (bytes)
   constexpr int QG = CO_T / 4;
-  constexpr int KG = PT * CO_T / 4 / 256;  // gy float4 items per thread per tile
-  constexpr int KH = (T::HALO * 8 + 255) / 256;
+  constexpr int NTH = NWCO * 2 * KSPLIT * 64;   // threads per block
+  constexpr int KG = PT * CO_T / 4 / NTH;  // gy float4 items per thread per tile
+  constexpr int KH = (T::HALO * 8 + NTH - 1) / NTH;
   constexpr int NIT = KG + KH;
   constexpr int KSTEPS = PT / 32;
   constexpr int NSLOT = (KSTEPS / KSPLIT) * 9;   // (k-step, tap) slots per wave and tile
@@ -734,7 +752,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_pipe_kernel(
   constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_UP);
   constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
   static_assert(T::NI == 1 && T::HP == 10 && T::WP == 10, "8x8 tiles");
-  static_assert(NWCO * 2 * KSPLIT == 4, "4 waves per block");
+  static_assert(NWCO * 2 * KSPLIT == 4 || (NWCO == 4 && KSPLIT == 1), "4 or 8 waves per block");
   static_assert(KSTEPS % KSPLIT == 0 && NIT <= NSLOT, "item slots");
   static_assert(MODE != ACT_NORM_POOL, "pool-fed layers use the materialised activation");
   extern __shared__ __attribute__((aligned(16))) char wsm[];
@@ -771,14 +789,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_pipe_kernel(
   int gyo[KG], glo[KG];
 #pragma unroll
   for (int k = 0; k < KG; ++k) {
-    const int px = (tid + 256 * k) / QG, r = px / TW, c = px % TW;
+    const int px = (tid + NTH * k) / QG, r = px / TW, c = px % TW;
     gyo[k] = (r * W + c) * Cout + co0 + qg * 4;
     glo[k] = px * GSB + qg * 8;
   }
   int hdr[KH], hdc[KH], hlo[KH];   // row / column relative to the tile origin (-1 .. 8)
 #pragma unroll
   for (int k = 0; k < KH; ++k) {
-    const int pix = (tid + 256 * k) >> 3;
+    const int pix = (tid + NTH * k) >> 3;
     hdr[k] = pix < T::HALO ? pix / T::WP - 1 : -(1 << 20);   // dead item: never in range
     hdc[k] = pix % T::WP - 1;
     hlo[k] = pix * WGS_ASB + qh * 8;
@@ -1254,18 +1272,19 @@ static void launch_wgp(dim3 grid, hipStream_t s, const float* src, const float* 
                        float* wpart, float* bpart, int B, int H, int W, int cin, int cout,
                        const WgGeom& g, const float* gmax, int gmT) {
   constexpr int CO_T = NWCO * 32;
+  constexpr int NTH = NWCO * 2 * KSPLIT * 64;
   const size_t lds_img = 2 * (size_t)npc(NP) * ((size_t)64 * (CO_T * 2 + 32) + (size_t)100 * WGS_ASB);
   const size_t lds_fold = KSPLIT == 2 ? (size_t)2 * 72 * 64 * 4 : 0;
   size_t lds = lds_img;
   if (lds < lds_fold) lds = lds_fold;
-  if (lds < 256 * 4 * 8) lds = 256 * 4 * 8;
+  if (lds < (size_t)NTH * 4 * 8) lds = (size_t)NTH * 4 * 8;
   auto k = wgrad_pipe_kernel<NP, NWCO, KSPLIT, MODE>;
   static bool once = false;
   if (!once) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, (const float2*)st, gy, wpart, bpart, B, H, W,
+  hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, src, (const float2*)st, gy, wpart, bpart, B, H, W,
                      cin, cout, g, gmax, gmT);
 }
 
@@ -1279,6 +1298,13 @@ static void dispatch_wgp(int mode, bool narrow, dim3 grid, hipStream_t s, const 
       case ACT_NORM: launch_wgp<NP, 1, 2, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
       case ACT_UP: launch_wgp<NP, 1, 2, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
       default: launch_wgp<NP, 1, 2, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+    }
+  } else if (wg_pipe_cot(cout) == 128) {
+    switch (mode) {
+      case ACT_RAW: launch_wgp<NP, 4, 1, ACT_RAW>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_NORM: launch_wgp<NP, 4, 1, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_UP: launch_wgp<NP, 4, 1, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      default: launch_wgp<NP, 4, 1, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
     }
   } else {
     switch (mode) {

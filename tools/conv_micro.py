@@ -48,6 +48,8 @@ CASES = {
     "wgrad32u": ("wgrad", 128, 32, 32, ACT_NORM_UP),
     "wgrad64": ("wgrad", 64, 64, 64, ACT_NORM),
     "wgrad128": ("wgrad", 32, 128, 128, ACT_NORM),
+    "wgrad128s16": ("wgrad", 16, 128, 128, ACT_NORM),
+    "wgrad64to128": ("wgrad", 32, 64, 128, ACT_NORM),
 }
 
 
