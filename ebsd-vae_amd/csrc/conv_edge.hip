@@ -78,7 +78,10 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_kernel(
 // with all 9 taps.  The 9 per-tap partial sums go through an LDS row so every column can
 // gather its three horizontal neighbours; output rows complete one input row later
 // (rolling accumulators).  HBM traffic ~ (TH+2)/TH x the input.
-constexpr int ROWS_TH = 16;
+#ifndef EV_ROWS_TH
+#define EV_ROWS_TH 16
+#endif
+constexpr int ROWS_TH = EV_ROWS_TH;   // rows per band (a multiple of 3 minus 2)
 constexpr int ROWS_PS = 36;   // LDS pixel stride (floats) of the staged row
 
 template <bool NORM, bool FLIP>

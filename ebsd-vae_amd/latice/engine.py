@@ -251,7 +251,8 @@ def _empty(*shape, like):
 #            emits; where a layer has no fp16 kernel (8x8 weight gradient of an upsampled
 #            source) it takes bf16x6.
 # Split modes cover every conv layer the split kernels support (Cout in {32,64,128},
-# H*W >= 256, plus the 8x8 maps); the others (the 1->32 first conv) stay fp32.
+# H*W >= 256, plus the 8x8 maps); the 1->32 first conv is an fp32 VALU kernel in every mode
+# (ebsdvae_conv_first_fwd; EBSDVAE_FIRST_VALU=0: the fp32-MFMA kernel).
 PIECES_F16 = 16   # EBSDVAE_PIECES_F16 (include/ebsdvae.h)
 _PIECES = {"fp32": 0, "bf16x3": 2, "bf16x6": 3, "f16x3": 3}
 _FWD_PIECES = {"f16x3": PIECES_F16}   # forward-conv piece format where it differs
