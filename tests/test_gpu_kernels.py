@@ -629,6 +629,37 @@ def test_dgrad_fused_split_f16(cuda, cin, cout, H, pmode, gscale, wscale):
     assert np.array_equal(gmax.max(1), np.abs(host(g_prev)).reshape(B, -1).max(1))
 
 
+@pytest.mark.parametrize("cin,cout,H", [(32, 64, 64), (64, 128, 32), (128, 128, 16), (128, 128, 8)])
+def test_pooled_reduce_matches_window_reduce(cuda, cin, cout, H):
+    """The fused InstanceNorm-backward reduce of a max-pooled block read from the pooled raw
+    output in identity mode (engine.conv_dgrad(..., ypool=)) == the reduce over the 2x2
+    windows of y (first argmax): the same input gradient bit for bit and the same finalized
+    {m1, m2} (only the window maximum gets gradient, and x-hat at it is (ypool - mean) * rstd)."""
+    rng = np.random.default_rng(61 + cin + cout + H)
+    B = 2
+    y = rng.standard_normal((B, 2 * H, 2 * H, cin)) * 2 + 0.5
+    _, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    ypool = y.reshape(B, H, 2, H, 2, cin).max(axis=(2, 4))
+    gy = rng.standard_normal((B, H, H, cout))
+    wsrc = rng.standard_normal((cout, cin, 3, 3)) * 0.05
+    layer = E.ConvLayer("t", E.KIND_CONV, cin, cout, H, E.ACT_RAW, 0)
+    with E.precision("f16x3"):
+        y_d, st_d, w_d = dev(y), dev(st), dev(wsrc)
+        wd = _pack_f16_dgrad(w_d, layer)
+        outs = []
+        for yp in (None, dev(ypool)):
+            g_d = dev(gy)
+            g_d.ev_gmax = dev(np.abs(gy).reshape(B, -1).max(1, keepdims=True))
+            gin, part = E.conv_dgrad(g_d, layer, w_d, prev=(y_d, st_d, E.P_POOL), wd=wd, ypool=yp)
+            g_prev = E.in_backward(gin, E.P_POOL, y_d, st_d, part=part)
+            torch.cuda.synchronize()
+            outs.append((gin, g_prev))
+    assert torch.equal(outs[0][0], outs[1][0])
+    # {m1, m2} agree to the last bits of the double sums, so the applied gradient does too
+    assert O.rel_err(host(outs[1][1]), host(outs[0][1])) < 1e-6
+
+
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16x6"])
 @pytest.mark.parametrize("cin,cout,H,mode,kind", [c for c in WG_CASES if c[0] >= 32 and c[1] >= 32])
 def test_conv_wgrad_split_bf16(cuda, cin, cout, H, mode, kind, prec):
