@@ -359,7 +359,8 @@ class PackSet:
         return PackedW(t, np_)
 
     def _add(self, L, w, dgrad, descs, scaled=True):
-        pf = self._one(L, w, False, descs)
+        # the VALU first conv reads the weight as it is (no pack)
+        pf = None if _first_valu(L) else self._one(L, w, False, descs)
         pd = self._one(L, w, True, descs, scaled) if dgrad else None
         self.packs[L.name] = (pf, pd)
 
@@ -385,6 +386,11 @@ def pool_out_ok(layer: ConvLayer, wp) -> bool:
 # the first block's backward can recompute y0 from x bit-identically instead of re-reading it
 # (ebsdvae_in_bwd_first_apply_wgrad_rc).  EBSDVAE_FIRST_VALU=0: the fp32-MFMA conv + re-read.
 _FIRST_VALU = os.environ.get("EBSDVAE_FIRST_VALU", "1") != "0"
+
+
+def _first_valu(layer: ConvLayer) -> bool:
+    return (layer.cin == 1 and layer.cout == 32 and layer.src_mode == ACT_RAW and _FIRST_VALU
+            and N.call("ebsdvae_conv_first_stat_tiles", layer.H, layer.H) > 0)
 
 
 def _conv_first(x, layer: ConvLayer, w, b, B):
@@ -413,8 +419,7 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     producer side of that (ebsdvae_conv3x3_fwd_split_pooled)."""
     H = layer.H
     src_mode = layer.src_mode if mode is None else mode
-    if (layer.cin == 1 and layer.cout == 32 and src_mode == ACT_RAW and not keep_act
-            and not pool_out and _FIRST_VALU and N.call("ebsdvae_conv_first_stat_tiles", H, H) > 0):
+    if src_mode == ACT_RAW and not keep_act and not pool_out and _first_valu(layer):
         return _conv_first(src, layer, w, b, B)
     if wp is None:
         wp = pack_weight(w, layer, dgrad=False)
@@ -876,7 +881,7 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True):
     for i, L in enumerate(plan.enc):
         w, b = params[L.name + ".weight"], params[L.name + ".bias"]
         wp = _wp(packs, L.name, 0)
-        if wp is None:
+        if wp is None and not _first_valu(L):
             wp = pack_weight(w, L, dgrad=False)
         nxt = plan.enc[i + 1] if i + 1 < len(plan.enc) else None
         # producer of a max-pool-fed layer: emit the pooled raw output in the epilogue, so

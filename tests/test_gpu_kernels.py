@@ -439,6 +439,9 @@ def test_batched_weight_pack_matches_single_packs(cuda):
     for i, L in enumerate(plan.enc + plan.dec):
         w = params[L.name + ".weight"]
         pf, pd = packs[L.name]
+        if pf is None:   # the VALU first conv reads its weight unpacked
+            assert L.cin == 1 and i == 0, L.name
+            continue
         single = E.pack_weight(w, L, dgrad=False)
         assert pf.pieces == single.pieces and torch.equal(pf.t, single.t), L.name
         if pd is not None:
