@@ -1001,10 +1001,20 @@ def heads_backward(plan: Plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, param
            N.ptr(eps), N.ptr(params["mu.0.weight"]), N.ptr(params["logvar.0.weight"]),
            N.ptr(params["linear2.0.weight"]), N.ptr(g_enc), N.ptr(gs), B, C, s, L, N.stream())
     out = {n: _grad_buf(grads, n, params[n]) for n in HEAD_NAMES}
-    nbytes = N.call("ebsdvae_heads_wgrad_work", B, F, L)
-    work = torch.empty(nbytes // 4, dtype=torch.float32, device=g_dec.device)
-    N.call("ebsdvae_heads_wgrad", N.ptr(flat), N.ptr(z), N.ptr(gs),
-           *[N.ptr(out[n]) for n in HEAD_NAMES], N.ptr(work), B, F, L, N.stream())
+    # the heads' weight gradients are off the critical path (g_enc is all the encoder
+    # backward needs): on the side stream inside deferred_side_join() (the trainer's step)
+    side = _side_stream(g_dec.device) if _DEFER else None
+    ctx = contextlib.nullcontext()
+    if side is not None:
+        side = _side_use(g_dec.device, flat, z, gs)
+        ctx = torch.cuda.stream(side)
+    with ctx:
+        nbytes = N.call("ebsdvae_heads_wgrad_work", B, F, L)
+        work = torch.empty(nbytes // 4, dtype=torch.float32, device=g_dec.device)
+        N.call("ebsdvae_heads_wgrad", N.ptr(flat), N.ptr(z), N.ptr(gs),
+               *[N.ptr(out[n]) for n in HEAD_NAMES], N.ptr(work), B, F, L, N.stream())
+    if side is not None:
+        _KEEP[_dev_key(g_dec.device)].append(work)
     return g_enc, out
 
 
@@ -1078,16 +1088,27 @@ def _decoder_backward(plan, g_xhat, saved, params, grads, packs):
 
 # ----------------------------------------------------------------------------- loss
 def loss_forward(x_hat, x, z, mu, std, kl_lambda: float):
-    """Returns (loss, kl_loss, recon_loss) 0-d tensors and per-sample (elbo, kl, recon)."""
+    """Returns (loss, kl_loss, recon_loss) 0-d tensors and per-sample (elbo, kl, recon).
+    Inside deferred_side_join() it runs on the side stream: the loss backward does not read
+    the loss values, so they are off the critical path (ready at the block's join)."""
     B = x_hat.shape[0]
     P = x_hat[0].numel()
     L = z.shape[1]
+    # outputs allocated on the current stream (the caller's), written on the side stream and
+    # kept alive until the join
     elbo, kl, recon = _empty(B, like=x_hat), _empty(B, like=x_hat), _empty(B, like=x_hat)
     loss, kl_loss, recon_loss = (torch.empty((), dtype=torch.float32, device=x_hat.device)
                                  for _ in range(3))
-    N.call("ebsdvae_vae_loss_fwd", N.ptr(x_hat), N.ptr(x), N.ptr(z), N.ptr(mu), N.ptr(std),
-           float(kl_lambda), N.ptr(elbo), N.ptr(kl), N.ptr(recon), N.ptr(loss), N.ptr(kl_loss),
-           N.ptr(recon_loss), B, P, L, N.stream())
+    side = _side_stream(x_hat.device) if _DEFER else None
+    ctx = contextlib.nullcontext()
+    if side is not None:
+        side = _side_use(x_hat.device, x_hat, x, z, mu, std, elbo, kl, recon, loss, kl_loss,
+                         recon_loss)
+        ctx = torch.cuda.stream(side)
+    with ctx:
+        N.call("ebsdvae_vae_loss_fwd", N.ptr(x_hat), N.ptr(x), N.ptr(z), N.ptr(mu), N.ptr(std),
+               float(kl_lambda), N.ptr(elbo), N.ptr(kl), N.ptr(recon), N.ptr(loss), N.ptr(kl_loss),
+               N.ptr(recon_loss), B, P, L, N.stream())
     return (loss, kl_loss, recon_loss), (elbo, kl, recon)
 
 

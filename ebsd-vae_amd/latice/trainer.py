@@ -125,12 +125,13 @@ class VAETrainer:
         eps = self._noise(x.shape[0]) if eps is None else eps
         flat, mu, std, z, dec_in = E.heads_forward(plan, enc, P, eps)
         x_hat, sd = E.decoder_forward(plan, dec_in, P, packs=packs)
-        (loss, kl, rec), _ = E.loss_forward(x_hat, x, z, mu, std, self.kl_lambda)
-        g_xhat, g_z, g_mu, g_std, _ = E.loss_backward(x_hat, x, z, mu, std, self.kl_lambda,
-                                                      g_loss=self.one, scale=1.0 / self.world)
-        # the weight-gradient side stream is joined once, after the encoder backward: the
-        # decoder's slice reductions finish on it while the encoder backward runs
+        # the side stream (weight gradients, their slice reductions, the heads' weight
+        # gradients, the loss values) is joined once, after the encoder backward: only the
+        # chain loss backward -> input gradients -> ... stays on the current stream
         with E.deferred_side_join(x.device):
+            (loss, kl, rec), _ = E.loss_forward(x_hat, x, z, mu, std, self.kl_lambda)
+            g_xhat, g_z, g_mu, g_std, _ = E.loss_backward(x_hat, x, z, mu, std, self.kl_lambda,
+                                                          g_loss=self.one, scale=1.0 / self.world)
             _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
             g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P,
                                         grads=G)
