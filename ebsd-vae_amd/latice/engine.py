@@ -547,6 +547,14 @@ def side_stream(device):
     return _SIDE[key]
 
 
+def side_streams_enabled() -> bool:
+    """Work may go to the side stream now (not disabled, not inside serial_streams(), and not
+    a capture that keeps everything on one stream)."""
+    if not _WG_STREAM or _SERIAL:
+        return False
+    return _GRAPH_SIDE or not torch.cuda.is_current_stream_capturing()
+
+
 def _side_stream(device):
     if not _WG_STREAM or _SERIAL:
         return None
@@ -870,16 +878,21 @@ def _wp(packs, name, k):
     return None if packs is None else packs[name][k]
 
 
-def encoder_forward(plan: Plan, x, params, packs=None, train=True):
+def encoder_forward(plan: Plan, x, params, packs=None, train=True, packs_ready=None):
     """x: (B,1,S,S) fp32 (== NHWC).  Returns (enc_out NHWC (B,s,s,C), saved).
     packs: PackSet.refresh() result (None: pack each weight on the fly).
-    train=False (inference): skip the pooled activations only the weight gradient needs."""
+    train=False (inference): skip the pooled activations only the weight gradient needs.
+    packs_ready: called once before the first layer that reads `packs` (the trainer packs on
+    the side stream while the unpacked VALU first conv runs)."""
     B = x.shape[0]
     saved = {}
     src, sst = x, None
     pooled = None   # the previous layer's max-pooled raw output, when it emitted one
     for i, L in enumerate(plan.enc):
         w, b = params[L.name + ".weight"], params[L.name + ".bias"]
+        if packs_ready is not None and not (i == 0 and _first_valu(L)):
+            packs_ready()
+            packs_ready = None
         wp = _wp(packs, L.name, 0)
         if wp is None and not _first_valu(L):
             wp = pack_weight(w, L, dgrad=False)

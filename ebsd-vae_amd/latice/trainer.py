@@ -120,9 +120,22 @@ class VAETrainer:
         """fwd + loss + bwd into self.gflat (+ the DP gradient exchange).  Returns the three
         loss scalars (device tensors)."""
         plan, P, G = self.plan, self.P, self.G
-        packs = self.packset.refresh()   # one launch packs every conv weight of the step
-        enc, se = E.encoder_forward(plan, x, P, packs=packs)
-        eps = self._noise(x.shape[0]) if eps is None else eps
+        # one launch packs every conv weight of the step, and the reparameterisation noise is
+        # drawn: both on the side stream, beside the first conv (which reads its weight
+        # unpacked); the current stream waits for them before the first packed layer
+        side = E.side_stream(x.device) if E.side_streams_enabled() else None
+        if side is not None:
+            main = torch.cuda.current_stream(x.device)
+            E.stream_wait(side, main)
+            with torch.cuda.stream(side):
+                packs = self.packset.refresh()
+                eps = self._noise(x.shape[0]) if eps is None else eps
+            ready = lambda: E.stream_wait(main, side)   # noqa: E731
+        else:
+            packs = self.packset.refresh()
+            eps = self._noise(x.shape[0]) if eps is None else eps
+            ready = None
+        enc, se = E.encoder_forward(plan, x, P, packs=packs, packs_ready=ready)
         flat, mu, std, z, dec_in = E.heads_forward(plan, enc, P, eps)
         x_hat, sd = E.decoder_forward(plan, dec_in, P, packs=packs)
         # the side stream (weight gradients, their slice reductions, the heads' weight
