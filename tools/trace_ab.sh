@@ -3,7 +3,6 @@
 # Usage: bash tools/trace_ab.sh TAG [VAR=VALUE ...]
 T=$1; shift
 export TMPDIR=/tmp
-env "$@" true
 for kv in "$@"; do export "$kv"; done
 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tab_$T -o run -- \
   python3 bench.py --steps 8 --warmup 3 --no-probe --no-cpu-baseline --strict-fp32-steps 0 \
