@@ -333,6 +333,53 @@ def strict_fp32_rate(model, x, args, dev, world):
             "dtype": "fp32"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: start N fresh child processes of this script, one per
+    GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in their environment, as
+    torch.distributed.run sets them), wait for all of them and return the worst exit code.
+    The parent never touches HIP (torch.cuda.device_count() does not initialise it), so the
+    children start on an untouched device; rank 0's JSON line goes to the shared stdout."""
+    import signal
+    import subprocess
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and ndev and args.gpus > ndev:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but only {ndev} visible GPU(s)")
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), EBSDVAE_BENCH_LAUNCHER="bench.py --gpus")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in pending:          # a failed rank would leave the others waiting
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -357,19 +404,37 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds before a stuck process-group init or collective raises")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:       # no launcher: spawn one rank per GPU, before any HIP call
+            sys.exit(launch_ranks(args))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started "
+                         f"WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; modulo only matters when rehearsing several ranks on one GPU
     local = local % max(1, torch.cuda.device_count())
+    pg = None
     if world > 1:
+        import datetime
         torch.cuda.set_device(local)
+        timeout = datetime.timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), timeout=timeout)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=timeout)
+        # what actually formed: the backend and the ranks of the group
+        pg = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
+              "launcher": os.environ.get("EBSDVAE_BENCH_LAUNCHER", "torch.distributed.run"),
+              "devices": min(world, max(1, torch.cuda.device_count())),
+              "timeout_s": args.dist_timeout}
+        if pg["world_size"] != world:
+            raise SystemExit(f"bench.py: process group has {pg['world_size']} ranks, expected {world}")
     dev = torch.device(f"cuda:{local}")
 
     from latice import engine as E
@@ -447,6 +512,8 @@ def main():
     step_tflops = step_flops_per_pattern(plan) * args.batch / (ms / 1e3) / 1e12
 
     prec = E.get_precision()
+    first_conv = ("fp32 VALU (one fixed fma chain, ebsdvae_conv_first_fwd)" if E._first_valu(plan.enc[0])
+                  else "fp32 MFMA (v_mfma_f32_32x32x2_f32)")
     res = {
         "metric": "EBSD patterns/sec (128x128, fwd+bwd)" if args.image_size == 128
         else f"EBSD patterns/sec ({args.image_size}x{args.image_size}, fwd+bwd)",
@@ -458,7 +525,7 @@ def main():
                   "f16x3": "fp32 I/O, f16x3 split MFMA"}[prec],
         "data": "synthetic",
         "conv_arithmetic": prec + {
-            "fp32": " (v_mfma_f32_32x32x2_f32 everywhere)",
+            "fp32": " (v_mfma_f32_32x32x2_f32; " + first_conv + " for the 1->32 conv)",
             "bf16x6": " (fp32 operands split into 3 bf16 pieces, 6 bf16 MFMA products per fp32"
                       " product, fp32 accumulation)",
             "bf16x3": " (2 bf16 pieces, 3 products: ~2^-16.5 per product)",
@@ -466,16 +533,20 @@ def main():
                      " product, ~2^-22.5, fp32 accumulation: forward, input-gradient and"
                      " weight-gradient convs; weights packed as w*2^k with one power of two per"
                      " layer from max|w|, the gradient operand scaled by a power of two per image"
-                     " (input gradient) or per slice (weight gradient); fp32 MFMA for the 1->32"
-                     " conv, bf16x6 for the 8x8 weight gradient fed by an upsample; all"
+                     " (input gradient) or per slice (weight gradient); " + first_conv +
+                     " for the 1->32 conv, bf16x6 for the 8x8 weight gradient fed by an upsample; all"
                      " activations, statistics and reductions fp32/fp64; passes the fp32 parity"
                      " gates, tests/test_gpu_trainer.py)"}[prec],
         "config": {"workload": f"c{2 if world == 1 else 3}: VariationalAutoEncoderRawData "
                                f"{args.image_size}x{args.image_size}, latent {args.latent_dim}, "
                                f"batch {args.batch}/GPU, fwd+loss+bwd+Adam"
-                               + (" + RCCL grad all-reduce" if world > 1 else ""),
+                               + (("" if pg is None else
+                                   " + RCCL grad all-reduce" if pg["backend"] == "nccl" else
+                                   f" + {pg['backend']} grad all-reduce (rehearsal, "
+                                   f"{pg['devices']} GPU(s))")),
                    "global_batch": world * args.batch, "image_size": args.image_size,
                    "latent_dim": args.latent_dim, "parallelism": f"dp{world}"},
+        "process_group": pg,
         "roofline": roof,
         "step_fp32_tflops": round(step_tflops, 2),
         "step_frac_of_fp32_peak": round(step_tflops / FP32_PEAK_TFLOPS, 4),

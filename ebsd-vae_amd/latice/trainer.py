@@ -27,13 +27,19 @@ from .functional import dec_param_names, enc_param_names
 class GradReducer:
     """Two-bucket asynchronous SUM all-reduce of a flat gradient buffer."""
 
-    def __init__(self, gflat: torch.Tensor, split: int, group=None):
+    def __init__(self, gflat: torch.Tensor, split: int, group=None, force: bool = False):
+        """force: issue the all-reduces even in a group of one rank (tests run the collective
+        path -- side-stream issue, wait ordering -- on a single GPU)."""
         self.gflat, self.split, self.group = gflat, split, group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        inited = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if inited else 1
+        if force and not inited:
+            raise RuntimeError("GradReducer(force=True) needs an initialised process group")
+        self.active = self.world > 1 or bool(force)
         self._works = []
 
     def start(self, bucket: int):
-        if self.world == 1:
+        if not self.active:
             return
         t = self.gflat[: self.split] if bucket == 0 else self.gflat[self.split:]
         self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
@@ -56,7 +62,7 @@ def shard_batch(x: torch.Tensor, rank: int, world: int) -> torch.Tensor:
 class VAETrainer:
     def __init__(self, model, kl_lambda: float = 5e-6, lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, amsgrad: bool = False,
-                 seed: int = 0, group=None):
+                 seed: int = 0, group=None, force_allreduce: bool = False):
         self.model = model
         self.plan = model.plan
         self.kl_lambda = float(kl_lambda)
@@ -94,7 +100,7 @@ class VAETrainer:
         self.step_count = torch.zeros((), device=dev, dtype=torch.float32)
         self.one = torch.ones((), device=dev, dtype=torch.float32)
         self.noise_counter = torch.zeros(1, device=dev, dtype=torch.int64)
-        self.reducer = GradReducer(self.gflat, self.split, group)
+        self.reducer = GradReducer(self.gflat, self.split, group, force=force_allreduce)
         self.world = self.reducer.world
         if self.world > 1:
             # every rank starts from rank 0's parameters (broadcast once
@@ -148,7 +154,7 @@ class VAETrainer:
             _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
             g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P,
                                         grads=G)
-            if self.world > 1:
+            if self.reducer.active:
                 # bucket 0 (decoder + heads) is complete on the side stream once it has
                 # caught up with the heads backward: the all-reduce is ordered behind it
                 side = E.side_stream(x.device)
