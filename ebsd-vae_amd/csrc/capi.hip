@@ -2,6 +2,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <mutex>
+
 #include "common.h"
 #include "../../include/ebsdvae.h"
 
@@ -37,27 +39,46 @@ extern "C" int ebsdvae_version(void) { return 1; }
 // system-scope writeback + invalidate of every fork / join costs the GPU a few microseconds of
 // idle time (tools/step_gaps.py).  A wait takes the event's state at enqueue time, so a small
 // ring of events per device is reused round-robin; capturable into hipGraphs (fork / join).
+// The ring is the signaler stream's device's (not the caller's current device), created
+// on that device; ring creation and the round-robin index are guarded, since forward and
+// autograd-backward threads both fork and join.
 extern "C" int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler) {
   constexpr int kRing = 64, kMaxDev = 64;
   static hipEvent_t ring[kMaxDev][kRing];
   static int next[kMaxDev];
   static bool made[kMaxDev];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
-    evh::set_error("stream_wait: no current device");
+  static std::mutex mu;
+  int dev = -1;
+  if (signaler == nullptr || hipStreamGetDevice((hipStream_t)signaler, &dev) != hipSuccess) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  if (dev < 0 || dev >= kMaxDev) {
+    evh::set_error("stream_wait: no device for the signaler stream");
     return 2;
   }
-  if (!made[dev]) {
-    for (int i = 0; i < kRing; ++i)
-      if (hipEventCreateWithFlags(&ring[dev][i], hipEventDisableTiming | hipEventReleaseToDevice) !=
-          hipSuccess) {
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if (!made[dev]) {
+      int cur = 0;
+      if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(dev) != hipSuccess) {
+        evh::set_error("stream_wait: cannot select device %d", dev);
+        return 2;
+      }
+      bool ok = true;
+      for (int i = 0; i < kRing && ok; ++i)
+        ok = hipEventCreateWithFlags(&ring[dev][i],
+                                     hipEventDisableTiming | hipEventReleaseToDevice) == hipSuccess;
+      (void)hipSetDevice(cur);
+      if (!ok) {
         evh::set_error("stream_wait: hipEventCreateWithFlags failed");
         return 2;
       }
-    made[dev] = true;
+      made[dev] = true;
+    }
+    ev = ring[dev][next[dev]];
+    next[dev] = (next[dev] + 1) % kRing;
   }
-  hipEvent_t ev = ring[dev][next[dev]];
-  next[dev] = (next[dev] + 1) % kRing;
   if (hipEventRecord(ev, (hipStream_t)signaler) != hipSuccess ||
       hipStreamWaitEvent((hipStream_t)waiter, ev, 0) != hipSuccess) {
     evh::set_error("stream_wait: %s", hipGetErrorString(hipGetLastError()));

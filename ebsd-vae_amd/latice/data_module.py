@@ -206,27 +206,81 @@ class DPdataset:
 class DeviceBatchLoader:
     """The DataLoader of the drop-in DPDataModule: batches of (patterns on the device,
     angles (B, 3) float64 tensor) over a subset of a DPdataset, in order or shuffled per
-    epoch (torch's default generator, as DataLoader(shuffle=True)).  A background thread
-    reads batch i+1 from the memmap into the second of two pinned buffers while batch i is
-    copied and transformed on the device; a buffer is refilled only after the device copy
-    out of it has completed (HIP event)."""
+    epoch.  A background thread reads batch i+1 from the memmap into the second of two
+    pinned buffers while batch i is copied and transformed on the device; a buffer is
+    refilled only after the device copy out of it has completed (HIP event).
+
+    Order, matching what the reference's `DataLoader(..., shuffle=...)` yields
+    (latice/data_module.py:215-261):
+      * one process: `DataLoader(shuffle=True)` draws its base seed and then RandomSampler's
+        seed from torch's default generator and permutes with a generator seeded by the
+        latter; the same draws happen here, so torch.manual_seed(s) gives the same epoch
+        order as the reference's loader.
+      * torch.distributed initialised with W > 1 ranks (Lightning DDP, which would inject a
+        DistributedSampler): each rank takes its DistributedSampler share -- the permutation
+        of a generator seeded with seed + epoch (seed = PL_GLOBAL_SEED, as Lightning passes
+        it, else 0), padded by wrapping to a multiple of W, then every W-th index from the
+        rank's offset -- so the ranks see disjoint batches that cover the epoch.
+        `set_epoch(e)` (reached through `.sampler`, where Lightning looks for it) moves to
+        epoch e."""
 
     def __init__(self, dataset: DPdataset, indices, batch_size: int, shuffle: bool = False,
-                 drop_last: bool = False):
+                 drop_last: bool = False, rank: int | None = None, world: int | None = None,
+                 seed: int | None = None):
         self.dataset = dataset
         self.indices = np.asarray(indices, dtype=np.int64)
         self.batch_size = int(batch_size)
         self.shuffle = bool(shuffle)
         self.drop_last = bool(drop_last)
+        if world is None:
+            import torch.distributed as dist
+            inited = dist.is_available() and dist.is_initialized()
+            world = dist.get_world_size() if inited else 1
+            rank = dist.get_rank() if inited else 0
+        self.rank, self.world = int(rank or 0), int(world)
+        if not 0 <= self.rank < self.world:
+            raise ValueError(f"rank {self.rank} outside a world of {self.world}")
+        import os
+        self.seed = int(os.environ.get("PL_GLOBAL_SEED", 0)) if seed is None else int(seed)
+        self.epoch = 0
+
+    @property
+    def sampler(self):
+        return self
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
+
+    def _num_local(self) -> int:
+        n = len(self.indices)
+        return n if self.world == 1 else math.ceil(n / self.world)
 
     def __len__(self) -> int:
-        n = len(self.indices)
+        n = self._num_local()
         return n // self.batch_size if self.drop_last else math.ceil(n / self.batch_size)
 
     def _order(self):
+        n = len(self.indices)
+        if self.world > 1:
+            # torch.utils.data.DistributedSampler (shuffle, drop_last=False)
+            if self.shuffle:
+                g = torch.Generator()
+                g.manual_seed(self.seed + self.epoch)
+                pos = torch.randperm(n, generator=g).numpy()
+            else:
+                pos = np.arange(n)
+            total = self._num_local() * self.world
+            if total > n:
+                pos = np.concatenate([pos] * (total // n) + [pos[: total % n]])
+            return self.indices[pos[self.rank:total:self.world]]
         if not self.shuffle:
             return self.indices
-        return self.indices[torch.randperm(len(self.indices)).numpy()]
+        # DataLoader.__iter__ draws its base seed, then RandomSampler.__iter__ its own seed
+        torch.empty((), dtype=torch.int64).random_()
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())
+        g = torch.Generator()
+        g.manual_seed(seed)
+        return self.indices[torch.randperm(n, generator=g).numpy()]
 
     def __iter__(self):
         order = self._order()

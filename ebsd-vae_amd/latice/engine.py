@@ -21,6 +21,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass, field
 
 import torch
@@ -207,6 +208,26 @@ def weights_written() -> None:
 
 def weights_generation() -> int:
     return _WEIGHTS_GEN
+
+
+# Deferred inference outputs (model.py: the decoder half of an eval/no-grad forward) that have
+# not been read yet.  Every raw-pointer weight writer calls before_weights_write() first, so
+# they are computed with the weights of the model(x) call that made them, as the reference
+# would have returned them then.
+_PENDING = weakref.WeakSet()
+
+
+def defer_until_weights_change(t) -> None:
+    _PENDING.add(t)
+
+
+def before_weights_write() -> None:
+    """Materialise every pending deferred value (called before a fused optimizer step or a
+    graph replay writes parameters through raw pointers)."""
+    while _PENDING:
+        for t in list(_PENDING):
+            _PENDING.discard(t)
+            t.materialize()
 
 
 # ----------------------------------------------------------------------------- state record

@@ -50,6 +50,23 @@ class IndexerConfig:
     orientation_threshold: float = 3.0
 
 
+def _default_db(dimension: int, device: torch.device):
+    """The reference's default store is `ChromaLatentVectorDatabase(dimension=...)`
+    (dp_indexer.py:73-77).  It is used when `latice.index.chroma_db` resolves (a reference
+    checkout on LATICE_REFERENCE_ROOT and chromadb installed); otherwise the HBM-resident
+    exact inner-product store `FaissLatentVectorDatabase` takes its place, with a warning
+    (same add / query API, exact instead of HNSW search)."""
+    try:
+        from latice.index.chroma_db import ChromaLatentVectorDatabase
+    except Exception as e:  # noqa: BLE001 - chromadb or the module absent
+        logger.warning("ChromaLatentVectorDatabase is not available (%s: %s); using the "
+                       "HBM-resident exact FaissLatentVectorDatabase as the default store",
+                       type(e).__name__, e)
+        return FaissLatentVectorDatabase(
+            FaissLatentVectorDatabaseConfig(dimension=dimension, device=str(device)))
+    return ChromaLatentVectorDatabase(dimension=dimension)
+
+
 class DiffractionPatternIndexer:
     """dp_indexer.py:51-297."""
 
@@ -62,9 +79,16 @@ class DiffractionPatternIndexer:
             logger.warning("CUDA not available, falling back to CPU")
             self.device = torch.device("cpu")
         logger.info(f"Using device: {self.device}")
-        self.db = db if db is not None else FaissLatentVectorDatabase(
-            FaissLatentVectorDatabaseConfig(dimension=self.config.latent_dim,
-                                            device=str(self.device)))
+        if self.device.type == "cpu" and isinstance(model, VariationalAutoEncoder):
+            # the drop-in model has no CPU path: IndexerConfig's default device "cpu" would
+            # only fail later, deep inside the first encode
+            if not torch.cuda.is_available():
+                raise RuntimeError("DiffractionPatternIndexer: the MI355X VAE needs a ROCm device "
+                                   "(config.device='cpu' and no GPU is visible; no CPU fallback)")
+            logger.warning("config.device='cpu': the drop-in VAE runs on the ROCm device; using "
+                           "cuda:%d", torch.cuda.current_device())
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.db = db if db is not None else _default_db(self.config.latent_dim, self.device)
         self.model = model
         self.model.eval()
         self.model.to(self.device)

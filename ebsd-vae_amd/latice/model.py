@@ -138,18 +138,31 @@ class VariationalAutoEncoder(nn.Module):
         _, mu, std, z, dec_in = E.heads_forward(plan, enc, params, eps.float().contiguous())
         versions = [(p, p._version) for p in params.values()]
         gen = E.weights_generation()
+        # the decoder may run later on another stream: it waits for this point of the stream
+        # that made dec_in (and the packs)
+        made_on = torch.cuda.current_stream(x.device)
+        ready = torch.cuda.Event()
+        ready.record(made_on)
 
         def decode():
+            # raw-pointer weight writers materialise pending values first
+            # (engine.before_weights_write); a torch in-place update bumps _version
             if gen != E.weights_generation() or any(p._version != v for p, v in versions):
                 raise RuntimeError("model parameters changed between model(x) and the first use "
                                    "of its deferred x_hat")
+            cur = torch.cuda.current_stream(x.device)
+            if cur != made_on:
+                cur.wait_event(ready)
+                dec_in.record_stream(cur)
             with torch.no_grad():
                 x_hat, _ = E.decoder_forward(plan, dec_in, params,
                                              packs=self._inference_packs(params))
             return x_hat
 
         S = plan.image_size
-        return z, DeferredTensor(decode, (x.shape[0], 1, S, S), torch.float32, x.device), mu, std
+        x_hat = DeferredTensor(decode, (x.shape[0], 1, S, S), torch.float32, x.device)
+        E.defer_until_weights_change(x_hat)
+        return z, x_hat, mu, std
 
     @torch.no_grad()
     def encode_mu(self, x: torch.Tensor) -> torch.Tensor:

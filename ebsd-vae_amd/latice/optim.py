@@ -28,6 +28,7 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        E.before_weights_write()
         for group in self.param_groups:
             b1, b2 = group["betas"]
             for p in group["params"]:

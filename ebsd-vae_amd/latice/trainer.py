@@ -168,6 +168,7 @@ class VAETrainer:
 
     def optimizer_step(self):
         b1, b2 = self.betas
+        E.before_weights_write()
         N.call("ebsdvae_adam", N.ptr(self.flat), N.ptr(self.gflat), N.ptr(self.exp_avg),
                N.ptr(self.exp_avg_sq), N.ptr(self.max_exp_avg_sq), N.ptr(self.step_count),
                self.flat.numel(), self.lr, float(b1), float(b2), self.adam_eps, self.weight_decay,
@@ -199,6 +200,7 @@ class VAETrainer:
         return out
 
     def replay(self):
+        E.before_weights_write()
         self.graph.replay()
         E.weights_written()
         return self._static[1]

@@ -130,3 +130,32 @@ def test_datamodule_loaders(cuda, tmp_path):
     assert np.array_equal(got, ref_x)
     t = create_default_transform((128, 128))
     assert np.array_equal(t(raw[3]).cpu().numpy(), ref_x[3])
+
+
+def test_deferred_value_survives_a_fused_optimizer_step(cuda):
+    """A pending x_hat is computed with the weights of the model(x) call that made it, even
+    when a fused Adam step (raw-pointer writes) runs before it is read, and when it is read
+    on another stream."""
+    from latice.optim import FusedAdam
+    m = _model(cuda)
+    x = torch.from_numpy(synthetic_patterns(4, 2)).to(cuda)
+    eps = torch.from_numpy(seeded_eps(4, 2)).to(cuda)
+    m.eval()
+    with torch.no_grad():
+        _, ref, _, _ = m(x, eps=eps)
+        ref = ref.detach().clone()
+        _, x_hat, _, _ = m(x, eps=eps)
+    assert not x_hat.materialized
+    opt = FusedAdam(m.parameters(), lr=1e-2)
+    for p in m.parameters():
+        p.grad = torch.ones_like(p)
+    opt.step()                                   # materialises x_hat first
+    assert x_hat.materialized
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        got = x_hat.detach().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    with torch.no_grad():                        # the new weights do change the output
+        _, x2, _, _ = m(x, eps=eps)
+        assert not torch.equal(x2.detach(), ref)
