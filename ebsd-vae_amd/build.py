@@ -46,11 +46,17 @@ def _stale(src: str, obj: str) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src: str, force: bool, objdir: str = OBJ, defines=()) -> str:
+# host-only AddressSanitizer flags: each -fsanitize= directly after -Xarch_host, so the device
+# code is built as usual (GPU ASan is not used)
+ASAN_HOST = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+
+def _compile(src: str, force: bool, objdir: str = OBJ, defines=(), extra=()) -> str:
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
     if force or _stale(src, obj):
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-               "-Wall", "-Wno-unused-function"] + [f"-D{d}" for d in defines] + ["-c", src, "-o", obj]
+               "-Wall", "-Wno-unused-function"] + list(extra) + [f"-D{d}" for d in defines] + \
+              ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -79,13 +85,41 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True, variant: str
     return LIB_
 
 
+def build_asan(jobs: int = 8, verbose: bool = True) -> str:
+    """Host-ASan build of the library objects linked into tests/asan/abi_asan.cpp, a driver
+    of the C ABI's argument validation, scratch-size queries and error plumbing (no GPU
+    needed).  Output: ebsd-vae_amd/build/asan/abi_asan (run by tests/test_abi.py)."""
+    objdir = os.path.join(OBJ, "asan")
+    os.makedirs(objdir, exist_ok=True)
+    drv = os.path.join(REPO, "tests", "asan", "abi_asan.cpp")
+    srcs = sources()
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, False, objdir, extra=ASAN_HOST + ["-g"]), srcs))
+    exe = os.path.join(objdir, "abi_asan")
+    if not os.path.exists(exe) or any(os.path.getmtime(d) > os.path.getmtime(exe)
+                                      for d in objs + [drv, HEADER]):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", "-x", "c++", drv,
+               "-x", "none"] + objs + ASAN_HOST + ["-fsanitize=address", "-o", exe + ".tmp"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"asan link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(exe + ".tmp", exe)
+    if verbose:
+        print(f"built {exe}")
+    return exe
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--variant", default="")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--asan", action="store_true", help="host-ASan C-ABI driver (tests/asan)")
     a = ap.parse_args()
+    if a.asan:
+        build_asan(a.j)
+        return
     build(a.j, a.force, variant=a.variant, defines=a.defines)
 
 

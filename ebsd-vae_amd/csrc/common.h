@@ -170,6 +170,9 @@ void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 }  // namespace evh
 
+// a spatial extent the shape queries accept (H * W and its multiples stay inside int)
+inline bool ev_dim_ok(int n) { return n > 0 && n <= 65536 && (long long)n * n <= (1LL << 30); }
+
 #define EV_REQUIRE(cond, ...)        \
   do {                               \
     if (!(cond)) {                   \

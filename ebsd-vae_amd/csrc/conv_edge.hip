@@ -316,7 +316,7 @@ using namespace ev;
 
 extern "C" int ebsdvae_conv_first_stat_tiles(int H, int W) {
   const int th = first_rows(W);
-  return (th > 0 && H % th == 0) ? H / th : -1;
+  return (th > 0 && ev_dim_ok(H) && H % th == 0) ? H / th : -1;
 }
 
 extern "C" int ebsdvae_conv_first_fwd(const float* x, const float* w0, const float* b0, float* y,

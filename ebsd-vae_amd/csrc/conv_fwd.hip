@@ -483,6 +483,7 @@ using namespace ev;
 
 // pixels per wave of the producing configuration -> InstanceNorm partial tiles per image
 extern "C" int ebsdvae_conv3x3_stat_tiles(int H, int W, int cout) {
+  if (!ev_dim_ok(H) || !ev_dim_ok(W)) return -1;
   const int MW = (H * W >= 256) ? (cout == 32 ? 128 : 64) : 32;
   return (H * W) / MW;
 }

@@ -1324,10 +1324,12 @@ extern "C" int ebsdvae_conv3x3_split_supported(int H, int W, int cin, int cout, 
 
 extern "C" int ebsdvae_conv3x3_split_stat_tiles(int H, int W, int cout) {
   (void)cout;
+  if (!ev_dim_ok(H) || !ev_dim_ok(W)) return -1;
   return (H * W) / 64;   // every split configuration writes one statistics slot per 64 pixels
 }
 
 extern "C" size_t ebsdvae_pack_split_bytes(int cin, int cout, int pieces) {
+  if (cin <= 0 || cout <= 0 || !(pieces == 2 || pieces == 3 || pieces == NP_F16)) return 0;
   return (size_t)(cin / XCK) * XTAPS * npc(pieces) * cout * XCK * 2 +
          (pieces == NP_F16 ? kF16PackTrailer : 0);
 }

@@ -58,6 +58,7 @@ static int wg_block_target(int pt) {
 
 // pt = pixels per tile (128 for fp32, 64 for the split-bf16 kernels)
 static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g, int pt = WG_PT) {
+  if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0) return false;
   const int twmax = pt == 64 && cout == 32 ? wg_tw_pref() : 32;
   g->TW = W < twmax ? W : twmax;
   if (H * g->TW >= pt) {
@@ -81,6 +82,7 @@ static bool wg_geom(int B, int H, int W, int cin, int cout, WgGeom* g, int pt = 
   // 8x8 maps (two-image tiles) use 32-wide co tiles: the 64-wide variant exceeds 256 VGPRs
   const int co_t = cout == 1 ? 1 : (cout == 32 || g->TW == 8 ? cout / 32 : cout / 64);
   const int ci_t = cin == 1 ? 1 : (cout == 1 ? 1 : cin / 32);
+  if (co_t <= 0 || ci_t <= 0) return false;
   const int want = wg_block_target(pt) / (co_t * ci_t);
   int tps = 4;
   while ((g->tiles + tps - 1) / tps > (want > 1 ? want : 1)) tps *= 2;
@@ -111,6 +113,7 @@ static int wg_pipe_cot(int cout) {
   return cout == 32 ? 32 : ((wide && cout % 128 == 0) ? 128 : 64);
 }
 static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
+  if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0) return false;
   if (H % 8 || W % 8 || cin % 32 || !(cout == 32 || cout % 64 == 0)) return false;
   g->TW = 8; g->TH = 8; g->NI = 1;
   g->ntx = W / 8; g->nty = H / 8;
@@ -1358,6 +1361,7 @@ using namespace ev;
 extern "C" int ebsdvae_conv3x3_wgrad_split_slices(int B, int H, int W, int cin, int cout, int pieces) {
   WgGeom g;
   if (pieces != 2 && pieces != 3 && pieces != NP_F16) return -1;
+  if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0) return -1;
   if (cin % 32 || !(cout == 32 || cout % 64 == 0)) return -1;
   if (pieces != 3 && wg_pipe()) return wg_pipe_geom(B, H, W, cin, cout, &g) ? g.slices : -1;
   const int pt = 64;

@@ -526,6 +526,7 @@ extern "C" int ebsdvae_upsample2_bwd(const float* g, float* out, int B, int H, i
 
 extern "C" int ebsdvae_in_bwd_tiles(int H, int W, int C) {
   (void)C;
+  if (!ev_dim_ok(H) || !ev_dim_ok(W)) return -1;
   return in_bwd_tiles_host(H, W);
 }
 
@@ -556,12 +557,14 @@ extern "C" int ebsdvae_in_bwd_finalize(const double* part, float* bstats, int B,
 // small maps still put >= 2048 workgroups (8 per CU) in flight
 static int in_bwd_apply_tiles_host(int B, int H, int W) {
   int T = in_bwd_tiles_host(H, W);
+  if (H <= 0) return T;
   while (B * T < 2048 && H % (2 * T) == 0 && ((H / (2 * T)) & 1) == 0) T *= 2;
   return T;
 }
 
 extern "C" int ebsdvae_in_bwd_apply_tiles(int B, int H, int W, int C) {
   (void)C;
+  if (B <= 0 || !ev_dim_ok(H) || !ev_dim_ok(W)) return -1;
   return in_bwd_apply_tiles_host(B, H, W);
 }
 
@@ -614,7 +617,9 @@ extern "C" int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, con
   return evh::check_launch("in_bwd_final_apply");
 }
 
-extern "C" int ebsdvae_in_bwd_final_tiles(int H, int W) { return in_bwd_tiles_host(H, W); }
+extern "C" int ebsdvae_in_bwd_final_tiles(int H, int W) {
+  return (ev_dim_ok(H) && ev_dim_ok(W)) ? in_bwd_tiles_host(H, W) : -1;
+}
 
 extern "C" int ebsdvae_in_bwd_final_apply_max(const float* g1, const float* w14, const float* y,
                                               const float* stats, const float* bstats, float* gy,

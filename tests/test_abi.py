@@ -61,3 +61,22 @@ def test_invalid_shapes_report_errors_without_gpu():
         _native.call("ebsdvae_conv3x3_fwd", 1, None, 0, 1, None, 1, None, None, 2, 16, 16, 3, 32, None)
     with pytest.raises(RuntimeError, match="null pointer"):
         _native.call("ebsdvae_heads_fwd", *([None] * 13), 2, 128, 4, 16, None)
+
+
+def test_host_asan_driver():
+    """the library's host code (argument validation, shape / scratch-size
+    queries, error strings, batched descriptors at and past their limits) under
+    AddressSanitizer: ebsd-vae_amd/build.py --asan links the library objects, built with
+    -Xarch_host -fsanitize=address, into tests/asan/abi_asan.cpp.  No GPU needed.
+    (__graft_entry__.build() builds it; here it is rebuilt only if stale.)"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "ebsd-vae_amd"))
+    import build
+    try:
+        exe = build.build_asan(verbose=False)
+    except RuntimeError as e:      # pragma: no cover - toolchain missing
+        pytest.skip(f"hipcc unavailable: {e}")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "AddressSanitizer" not in r.stderr, (r.stdout + r.stderr)[-4000:]
+    assert "abi_asan: ok" in r.stdout
