@@ -214,19 +214,25 @@ def weights_generation() -> int:
 # not been read yet.  Every raw-pointer weight writer calls before_weights_write() first, so
 # they are computed with the weights of the model(x) call that made them, as the reference
 # would have returned them then.
-_PENDING = weakref.WeakSet()
+_PENDING = {}   # id -> weakref (tensors compare elementwise, so no WeakSet)
 
 
 def defer_until_weights_change(t) -> None:
-    _PENDING.add(t)
+    key = id(t)
+
+    def gone(ref, key=key):
+        if _PENDING.get(key) is ref:
+            del _PENDING[key]
+    _PENDING[key] = weakref.ref(t, gone)
 
 
 def before_weights_write() -> None:
     """Materialise every pending deferred value (called before a fused optimizer step or a
     graph replay writes parameters through raw pointers)."""
     while _PENDING:
-        for t in list(_PENDING):
-            _PENDING.discard(t)
+        _, ref = _PENDING.popitem()
+        t = ref()
+        if t is not None:
             t.materialize()
 
 
