@@ -56,6 +56,17 @@ EV_DEVINL float first_conv_px(const float (&nb)[9], const float (&wt)[9], float 
   for (int t = 1; t < 9; ++t) s = fmaf(nb[t], wt[t], s);
   return s + bias;
 }
+// Two channels of first_conv_px at once on v_pk_fma_f32 (each lane of the pair runs exactly
+// first_conv_px's chain, so the values are bit-identical): w2[t] = the two channels' tap t.
+typedef float pkf2 __attribute__((ext_vector_type(2)));
+EV_DEVINL pkf2 pk2(float a, float b) { return pkf2{a, b}; }
+EV_DEVINL pkf2 pkfma(pkf2 a, pkf2 b, pkf2 c) { return __builtin_elementwise_fma(a, b, c); }
+EV_DEVINL pkf2 first_conv_px2(const float (&nb)[9], const pkf2 (&w2)[9], pkf2 b2) {
+  pkf2 s = pk2(nb[0], nb[0]) * w2[0];
+#pragma unroll
+  for (int t = 1; t < 9; ++t) s = pkfma(pk2(nb[t], nb[t]), w2[t], s);
+  return s + b2;
+}
 EV_DEVINL void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 EV_DEVINL float4 max4(float4 a, float4 b) {

@@ -253,12 +253,12 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
     const int gh = r0 - 1 + r, gw = cc - 1;
     xs[i] = (gh >= 0 && gh < H && gw >= 0 && gw < W) ? xb[gh * W + gw] : 0.f;
   }
-  float wt[4][9], bb[4];
+  pkf2 wt2[2][9], bb2[2];   // channel pairs (2k, 2k+1) for v_pk_fma_f32
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 2; ++k) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wt[k][t] = w0[(c + k) * 9 + t];
-    bb[k] = b0 ? b0[c + k] : 0.f;
+    for (int t = 0; t < 9; ++t) wt2[k][t] = pk2(w0[(c + 2 * k) * 9 + t], w0[(c + 2 * k + 1) * 9 + t]);
+    bb2[k] = b0 ? pk2(b0[c + 2 * k], b0[c + 2 * k + 1]) : pk2(0.f, 0.f);
   }
   __syncthreads();
   float v[FIRST_NPT][4];
@@ -270,10 +270,14 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
     float nb[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) nb[t] = xs[(h + t / 3) * WP + w + t % 3];
+    // two channels per v_pk_fma_f32 (bit-identical to first_conv_px per channel)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[j][k] = first_conv_px(nb, wt[k], bb[k]);
-      s[k] += v[j][k];
+    for (int k = 0; k < 2; ++k) {
+      const pkf2 y2 = first_conv_px2(nb, wt2[k], bb2[k]);
+      v[j][2 * k] = y2.x;
+      v[j][2 * k + 1] = y2.y;
+      s[2 * k] += y2.x;
+      s[2 * k + 1] += y2.y;
     }
     st4(yb + (size_t)p * FIRST_C, make_float4(v[j][0], v[j][1], v[j][2], v[j][3]));
   }

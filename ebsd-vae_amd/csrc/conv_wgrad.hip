@@ -797,13 +797,20 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
     glo[k] = px * GSB + qg * 8;
   }
   int hdr[KH], hdc[KH], hlo[KH];   // row / column relative to the tile origin (-1 .. 8)
+  int hbo[KH];                     // byte offset of the item relative to the tile's source origin
+  const int srow = Ws * Cin * 4;   // bytes per source row
 #pragma unroll
   for (int k = 0; k < KH; ++k) {
     const int pix = (tid + NTH * k) >> 3;
     hdr[k] = pix < T::HALO ? pix / T::WP - 1 : -(1 << 20);   // dead item: never in range
     hdc[k] = pix % T::WP - 1;
     hlo[k] = pix * WGS_ASB + qh * 8;
+    // UPS: (y0 + dr) >> 1 == y0 / 2 + (dr >> 1) for even y0 (arithmetic shift = floor)
+    hbo[k] = pix < T::HALO ? (UPS ? (hdr[k] >> 1) * srow + (hdc[k] >> 1) * Cin * 4
+                                  : hdr[k] * srow + hdc[k] * Cin * 4) + (ci0 + qh * 4) * 4
+                           : (int)0x80000000;   // dead item: out of range, never staged
   }
+  const int gimg_bytes = H * W * Cout * 4, simg_bytes = Hs * Ws * Cin * 4;
 
   float4 rg[KG], rh[KH];
   float2 st_l[4], st_s[4];         // NORM: stats of the loading / the staging tile's image
@@ -813,10 +820,25 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
     const int ib = t / per_img, rr = t - ib * per_img, ty = rr / g.ntx;
     b0 = ib; y0 = ty * T::TH; x0 = (rr - ty * g.ntx) * TW;
   };
+  // buffer loads with 32-bit offsets into the loading tile's image (scalar descriptor base,
+  // tile-uniform offset + a per-lane constant): rows above / below the image and dead items
+  // fall outside the descriptor's range and read 0 without a memory access; the left / right
+  // halo columns read a neighbouring row's pixel, which the staging zeroes (in_img)
+  __amdgpu_buffer_rsrc_t rgy, rsrc;
+  int gtoff = 0, stoff = 0;
+  auto set_tile = [&]() EV_LAMBDA_INLINE {
+    rgy = __builtin_amdgcn_make_buffer_rsrc((void*)(gy + (size_t)lb * H * W * Cout), 0, gimg_bytes,
+                                            0x00020000);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)lb * Hs * Ws * Cin), 0,
+                                             simg_bytes, 0x00020000);
+    gtoff = (ly * W + lx) * Cout * 4;
+    stoff = UPS ? (ly >> 1) * srow + (lx >> 1) * Cin * 4 : ly * srow + lx * Cin * 4;
+  };
   auto load_stats = [&]() EV_LAMBDA_INLINE {
-    if constexpr (NORM) {
+    set_tile();
+    if constexpr (NORM) {   // as {rstd, -mean*rstd}: one FMA + LeakyReLU per value
       const float2* sp = sstats + (size_t)lb * Cin + ci0 + qh * 4;
-      st_l[0] = sp[0]; st_l[1] = sp[1]; st_l[2] = sp[2]; st_l[3] = sp[3];
+      st_l[0] = norm_fs(sp[0]); st_l[1] = norm_fs(sp[1]); st_l[2] = norm_fs(sp[2]); st_l[3] = norm_fs(sp[3]);
     }
   };
   auto in_img = [&](int k, int y0, int x0) EV_LAMBDA_INLINE {
@@ -825,14 +847,14 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
   auto issue_item = [&](auto j_c) EV_LAMBDA_INLINE {
     constexpr int j = decltype(j_c)::value;
     if constexpr (j < KG) {
-      rg[j] = ld4(gy + ((size_t)lb * H + ly) * W * Cout + (size_t)lx * Cout + gyo[j]);
+      rg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rgy, gtoff + gyo[j] * 4, 0, 0));
     } else {
-      // unconditional, at a clamped address (the staging zeroes what lies outside the image):
-      // with every load issued, the compiler's vmcnt waits count exactly one tile's loads
+      // unconditional (the staging zeroes what lies outside the image): with every load
+      // issued, the compiler's vmcnt waits count exactly one tile's loads
       constexpr int k = j - KG;
-      const int sh = min(max(UPS ? (ly >> 1) + (hdr[k] >> 1) : ly + hdr[k], 0), Hs - 1);
-      const int sw = min(max(UPS ? (lx >> 1) + (hdc[k] >> 1) : lx + hdc[k], 0), Ws - 1);
-      rh[k] = ld4(src + (((size_t)lb * Hs + sh) * Ws + sw) * Cin + ci0 + qh * 4);
+      rh[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rsrc, stoff + hbo[k], 0, 0));
     }
   };
   float4 tb;   // this thread's gy sum of the staging tile (bias)
@@ -850,8 +872,8 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
         if (in_img(k, sy, sx)) {
           v = rh[k];
           if (NORM)
-            v = make_float4(normact(v.x, st_s[0]), normact(v.y, st_s[1]), normact(v.z, st_s[2]),
-                            normact(v.w, st_s[3]));
+            v = make_float4(normact_fs(v.x, st_s[0]), normact_fs(v.y, st_s[1]),
+                            normact_fs(v.z, st_s[2]), normact_fs(v.w, st_s[3]));
         }
         store_pieces<NP>(buf + NPC * GY_PIECE + hlo[k], ACT_PIECE, v);
       }

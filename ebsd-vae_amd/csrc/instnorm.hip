@@ -272,22 +272,24 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) { m1[k] = bp[k].x; m2[k] = bp[k].y; }
   }
-  float wv[4][9], bb0[4];   // FINAL: w14 (1, 32, 3, 3); RC: w0 (32, 1, 3, 3) and b0
+  // FINAL: w14 (1, 32, 3, 3); RC: w0 (32, 1, 3, 3) and b0 -- as channel pairs (2k, 2k+1) of
+  // this thread's 4 channels, for v_pk_fma_f32
+  pkf2 wv2[2][9], bb2[2];
   if (FUSE_ == FUSE_FINAL || RC) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 2; ++k) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wv[k][t] = w14[(c + k) * 9 + t];
-      bb0[k] = (RC && b0) ? b0[c + k] : 0.f;
+      for (int t = 0; t < 9; ++t) wv2[k][t] = pk2(w14[(c + 2 * k) * 9 + t], w14[(c + 2 * k + 1) * 9 + t]);
+      bb2[k] = (RC && b0) ? pk2(b0[c + 2 * k], b0[c + 2 * k + 1]) : pk2(0.f, 0.f);
     }
   }
   double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
-  float wacc[4][9];
+  pkf2 wacc2[2][9];   // weight-gradient partials of the channel pairs
   float bacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < 2; ++k)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wacc[k][t] = 0.f;
+    for (int t = 0; t < 9; ++t) wacc2[k][t] = pk2(0.f, 0.f);
   const float* yb = y + (size_t)b * H * W * C;
   // the 1-channel neighbour source (FINAL: g1, FIRST: x) of this row band plus its 1-pixel
   // halo, staged once in LDS with coalesced loads (zero padding at the image border)
@@ -360,12 +362,14 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     }
     float ga[4];
     if (FUSE_ == FUSE_FINAL) {
+      // two channels per v_pk_fma_f32 (per channel the same fma chain)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float s = 0.f;
+      for (int k = 0; k < 2; ++k) {
+        pkf2 s = pk2(0.f, 0.f);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) s = fmaf(nb[t], wv[k][t], s);
-        ga[k] = s;
+        for (int t = 0; t < 9; ++t) s = pkfma(pk2(nb[t], nb[t]), wv2[k][t], s);
+        ga[2 * k] = s.x;
+        ga[2 * k + 1] = s.y;
       }
       if (!APPLY && cg == 0) bacc[0] += nb[4];   // g1[p] itself (centre tap): db14
     } else {
@@ -376,9 +380,13 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     float yy[4] = {y4.x, y4.y, y4.z, y4.w};
     if (RC) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) yy[k] = first_conv_px(nb, wv[k], bb0[k]);
+      for (int k = 0; k < 2; ++k) {
+        const pkf2 y2 = first_conv_px2(nb, wv2[k], bb2[k]);
+        yy[2 * k] = y2.x;
+        yy[2 * k + 1] = y2.y;
+      }
     }
-    float o[4];
+    float o[4], av[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float xh = (yy[k] - mean[k]) * rstd[k];
@@ -386,18 +394,19 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       if (!APPLY) {
         a1[k] += (double)gx;
         a2[k] = fma((double)gx, (double)xh, a2[k]);
-        if (FUSE_ == FUSE_FINAL) {
-          const float av = lrelu(xh);
-#pragma unroll
-          for (int t = 0; t < 9; ++t) wacc[k][t] = fmaf(nb[t], av, wacc[k][t]);
-        }
+        av[k] = lrelu(xh);
       } else {
         o[k] = rstd[k] * (gx - m1[k] - xh * m2[k]);
-        if (FUSE_ == FUSE_FIRST) {
-          bacc[k] += o[k];
+        if (FUSE_ == FUSE_FIRST) bacc[k] += o[k];
+      }
+    }
+    // weight-gradient partials, two channels per v_pk_fma_f32 (per channel the same chain)
+    if ((FUSE_ == FUSE_FINAL && !APPLY) || (FUSE_ == FUSE_FIRST && APPLY)) {
 #pragma unroll
-          for (int t = 0; t < 9; ++t) wacc[k][t] = fmaf(o[k], nb[t], wacc[k][t]);
-        }
+      for (int k = 0; k < 2; ++k) {
+        const pkf2 f = (FUSE_ == FUSE_FINAL) ? pk2(av[2 * k], av[2 * k + 1]) : pk2(o[2 * k], o[2 * k + 1]);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wacc2[k][t] = pkfma(pk2(nb[t], nb[t]), f, wacc2[k][t]);
       }
     }
     if (APPLY && FUSE_ == FUSE_FINAL) {
@@ -442,7 +451,7 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        float v = wacc[k][t];
+        float v = (k & 1) ? wacc2[k >> 1][t].y : wacc2[k >> 1][t].x;
         wave_fold8(v);
         if (lane < CG) wred[wave][lane][k * 9 + t] = v;
       }

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--image-size", type=int, default=128)
     ap.add_argument("--latent-dim", type=int, default=16)
+    ap.add_argument("--serial", action="store_true",
+                    help="weight gradients on the main stream (each launch timed alone)")
     a = ap.parse_args()
     m = VariationalAutoEncoderRawData(32, a.latent_dim, a.image_size)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in
@@ -33,7 +35,8 @@ def main():
     x = torch.from_numpy(synthetic_patterns(0, a.batch, a.image_size)).cuda()
     for _ in range(2):
         tr.step(x)
-    with E.probe() as pr:
+    import contextlib
+    with E.probe() as pr, (E.serial_streams() if a.serial else contextlib.nullcontext()):
         for _ in range(a.steps):
             tr.step(x)
     rows = sorted(pr.per_tag().items(), key=lambda kv: -kv[1][2])
