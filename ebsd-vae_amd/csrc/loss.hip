@@ -58,6 +58,32 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(
   }
 }
 
+// As loss_fwd_kernel with the BCE sums already reduced per row band by ebsdvae_net_end:
+// recon_b = sum_t bce_part[b][t] / P (fixed order).
+__global__ __launch_bounds__(64) void loss_fwd_parts_kernel(
+    const float* __restrict__ bce_part, int T, const float* __restrict__ z,
+    const float* __restrict__ mu, const float* __restrict__ sd, float lam,
+    float* __restrict__ elbo, float* __restrict__ kl, float* __restrict__ recon, int P, int L) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  float k = 0.f;
+  for (int j = tid; j < L; j += 64) {
+    const size_t bj = (size_t)b * L + j;
+    const float zz = z[bj], m = mu[bj], sdv = sd[bj];
+    const float d = (zz - m) / sdv;
+    k += 0.5f * zz * zz - 0.5f * d * d - logf(sdv);
+  }
+  k = wave_sum(k);
+  if (tid == 0) {
+    float r = 0.f;
+    for (int t = 0; t < T; ++t) r += bce_part[(size_t)b * T + t];
+    const float rs = r / (float)P;
+    const float ks = lam * (k / (float)L);
+    recon[b] = rs;
+    kl[b] = ks;
+    elbo[b] = ks + rs;
+  }
+}
+
 __global__ __launch_bounds__(256) void loss_mean_kernel(const float* __restrict__ elbo,
                                                         const float* __restrict__ kl,
                                                         const float* __restrict__ recon,
@@ -96,7 +122,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   const int i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
   const float* xb = xh + (size_t)b * P;
   const float* yb = x + (size_t)b * P;
-  if (i0 < P) {
+  if (gxh && i0 < P) {   // gxh NULL: the logit gradient comes from ebsdvae_net_end
     if (i0 + 4 <= P && (P & 3) == 0) {
       const float4 a = ld4(xb + i0), t = ld4(yb + i0);
       st4(gxh + (size_t)b * P + i0,
@@ -147,12 +173,27 @@ extern "C" int ebsdvae_vae_loss_bwd(const float* x_hat, const float* x, const fl
                                     const float* g_recon_loss, const float* g_elbo, float scale,
                                     float* g_xhat, float* g_z, float* g_mu, float* g_std,
                                     float* g_x, int B, int P, int L, ebsdvae_stream_t stream) {
-  EV_REQUIRE(x_hat && x && z && mu && std && g_xhat && g_z && g_mu && g_std,
+  EV_REQUIRE(z && mu && std && g_z && g_mu && g_std && (!g_xhat || (x_hat && x)),
              "vae_loss_bwd: null pointer");
   EV_REQUIRE(B > 0 && P > 0 && L > 0 && L <= 256, "vae_loss_bwd: bad shape");
-  const int bx = (P / 4 + 255) / 256 + 1;
+  const int bx = g_xhat ? (P / 4 + 255) / 256 + 1 : 1;
   hipLaunchKernelGGL(loss_bwd_kernel, dim3(bx, B), dim3(256), 0, (hipStream_t)stream, x_hat, x, z,
                      mu, std, kl_lambda, g_loss, g_kl_loss, g_recon_loss, g_elbo, scale, g_xhat,
                      g_z, g_mu, g_std, g_x, B, P, L);
   return evh::check_launch("vae_loss_bwd");
+}
+
+extern "C" int ebsdvae_vae_loss_fwd_parts(const float* bce_part, int tiles, const float* z,
+                                          const float* mu, const float* std, float kl_lambda,
+                                          float* elbo, float* kl, float* recon, float* loss,
+                                          float* kl_loss, float* recon_loss, int B, int P, int L,
+                                          ebsdvae_stream_t stream) {
+  EV_REQUIRE(bce_part && z && mu && std && elbo && kl && recon && loss && kl_loss && recon_loss,
+             "vae_loss_fwd_parts: null pointer");
+  EV_REQUIRE(B > 0 && P > 0 && L > 0 && L <= 256 && tiles > 0, "vae_loss_fwd_parts: bad shape");
+  hipLaunchKernelGGL(loss_fwd_parts_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, bce_part, tiles,
+                     z, mu, std, kl_lambda, elbo, kl, recon, P, L);
+  hipLaunchKernelGGL(loss_mean_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, elbo, kl, recon,
+                     loss, kl_loss, recon_loss, B);
+  return evh::check_launch("vae_loss_fwd_parts");
 }

@@ -1,0 +1,310 @@
+// Network end of the training step in ONE pass over the last block's pre-norm output y13:
+//   x_hat = Conv2d(32, 1)(lrelu(IN(y13)))                        latice/model.py:147-148
+//   BCE-with-logits per-sample sums, and its logit gradient       lightning_module.py:79-92
+//     g1 = d loss / d x_hat = g_loss * scale / (B * P) * (sigmoid(x_hat) - x)
+//   the InstanceNorm-backward reduce of that block (sum g_a*lrelu', sum g_a*lrelu'*xhat per
+//   (b, c), g_a = the final conv's input gradient recomputed from g1) and the final conv's
+//   weight / bias gradient partials                                (autograd of :147-148)
+// These were three kernels that each read y13 (512 MB at B = 256): the 32 -> 1 conv, the loss
+// (x_hat, x) and the fused final reduce (in_bwd_edge_kernel<FUSE_FINAL, false>).  The apply
+// pass that writes the block's output gradient (ebsdvae_in_bwd_final_apply_max) reads g1 from
+// here and is unchanged.
+//
+// Block = one band of TH output rows of one image (W = 128: 8 channel groups x 32 pixel lanes,
+// 4 pixels per thread per row).  It streams the source rows r0-2 .. r0+TH+1 once: row q is
+// normalised into a 4-row ring of a = lrelu(IN(y13)) in LDS; x_hat / g1 of row q-1 follow from
+// the ring (g1 into a 4-row ring); the reduce of row q-2 from the g1 ring and a.  Four slots
+// let every step write the slot of a row the previous step no longer reads, so two barriers
+// per row suffice.  The two halo
+// rows above and below are recomputed by the neighbouring bands (x_hat / g1 are written only
+// for the band's own rows).  The sums are fp32 per row and thread, double across rows, lanes
+// and waves (fixed order), as the reduce kernel it replaces.
+#include "common.h"
+#include "../../include/ebsdvae.h"
+
+namespace ev {
+
+constexpr int NE_C = 32, NE_W = 128, NE_TH = 16, NE_NTH = 256;
+constexpr int NE_WP = NE_W + 2;            // ring row: zero column, W pixels, zero column
+constexpr int NE_AROW = NE_WP * NE_C;      // floats per a-ring row
+constexpr int NE_RING = 4;                 // ring slots (a and g1): slot(row) = (row - r0 + k) & 3
+
+EV_DEVINL float ne_bce(float xh, float t) {
+  return (1.f - t) * xh + fmaxf(-xh, 0.f) + log1pf(expf(-fabsf(xh)));
+}
+EV_DEVINL float ne_sigmoid(float x) {
+  if (x >= 0.f) return 1.f / (1.f + expf(-x));
+  const float e = expf(x);
+  return e / (1.f + e);
+}
+// sum over the 8 channel-group lanes of a pixel (lanes 8k .. 8k+7), on the VALU through DPP:
+// quad_perm [1,0,3,2] (xor 1), [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7 - i,
+// which pairs the two quads of the 8-lane group)
+template <int CTRL>
+EV_DEVINL float ne_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+EV_DEVINL float ne_fold8(float v) {
+  v += ne_dpp<0xB1>(v);
+  v += ne_dpp<0x4E>(v);
+  v += ne_dpp<0x141>(v);
+  return v;
+}
+
+__global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
+    const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
+    const float* __restrict__ b14, const float* __restrict__ xt, const float* __restrict__ g_loss,
+    float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
+    double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
+  constexpr int C = NE_C, W = NE_W, TH = NE_TH, WP = NE_WP;
+  extern __shared__ __attribute__((aligned(16))) float ne_sm[];
+  float* aring = ne_sm;                       // [4][WP][C]
+  float* gring = ne_sm + NE_RING * NE_AROW;   // [4][WP]
+  const int tile = blockIdx.x, b = blockIdx.y, T = gridDim.x;
+  const int tid = threadIdx.x, cg = tid & 7, pl = tid >> 3;
+  const int c = cg * 4;
+  const int r0 = tile * TH;
+  const size_t HW = (size_t)H * W;
+
+  float2 fs[4];   // {rstd, -mean * rstd}
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fs[k] = norm_fs(st[(size_t)b * C + c + k]);
+  pkf2 wv2[2][9];   // w14 (1, 32, 3, 3) as channel pairs (c, c+1), (c+2, c+3)
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wv2[k][t] = pk2(w14[(c + 2 * k) * 9 + t], w14[(c + 2 * k + 1) * 9 + t]);
+  const float bias = b14 ? b14[0] : 0.f;
+  const float cr = gscale * (g_loss ? *g_loss : 1.f);   // g_loss * scale / (B * P)
+
+  // zero columns of both rings (never written by the row passes)
+  for (int i = tid; i < NE_RING * 2 * (C / 4); i += NE_NTH) {
+    const int r = i / (2 * (C / 4)), side = (i / (C / 4)) & 1, q4 = i % (C / 4);
+    st4(aring + r * NE_AROW + side * (W + 1) * C + q4 * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+  }
+  if (tid < 2 * NE_RING) gring[(tid >> 1) * WP + (tid & 1) * (W + 1)] = 0.f;
+
+  const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + (size_t)b * HW * C), 0,
+                                                    (int)(HW * C * 4), 0x00020000);
+  // row q of y13 for this thread: 4 pixels pl + 32 j, channels c .. c+3 (out-of-image rows
+  // fall outside the buffer range and read 0; they are zeroed as conv padding anyway)
+  auto load_row = [&](int q, float4 (&d)[4]) EV_LAMBDA_INLINE {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      d[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            ry, ((q * W + pl + 32 * j) * C + c) * 4, 0, 0));
+  };
+
+  double s1d[4] = {0.0, 0.0, 0.0, 0.0}, s2d[4] = {0.0, 0.0, 0.0, 0.0};
+  pkf2 wacc2[2][9];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wacc2[k][t] = pk2(0.f, 0.f);
+  float bsum = 0.f, bce = 0.f;   // g1 and BCE sums over the band (cg == 0 lanes)
+
+  // the BCE target of x_hat row r0 - 3 + i, loaded two steps ahead (its pixels pl + 32 j)
+  auto load_tgt = [&](int r, float (&d)[4]) EV_LAMBDA_INLINE {
+    const bool in = r >= 0 && r < H;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = in ? xt[(size_t)b * HW + (size_t)r * W + pl + 32 * j] : 0.f;
+  };
+  float4 ybuf[2][4];
+  float tbuf[2][4];
+  load_row(r0 - 2, ybuf[0]);
+  load_row(r0 - 1, ybuf[1]);
+  load_tgt(r0 - 3, tbuf[0]);
+  load_tgt(r0 - 2, tbuf[1]);
+  __syncthreads();   // ring columns zeroed
+
+  auto step = [&](int i, float4 (&ycur)[4], float (&tcur)[4]) EV_LAMBDA_INLINE {
+    const int q = r0 - 2 + i;
+    // (1) a = lrelu(IN(y13)) of source row q into ring slot i & 3 (zero outside the image)
+    {
+      float* ar = aring + (i & 3) * NE_AROW;
+      const bool in = q >= 0 && q < H;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float4 v = ycur[j];
+        v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]), normact_fs(v.z, fs[2]),
+                        normact_fs(v.w, fs[3]));
+        if (!in) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        st4(ar + (pl + 32 * j + 1) * C + c, v);
+      }
+    }
+    // prefetch row q + 2 into the registers just consumed
+    load_row(q + 2, ycur);
+    __syncthreads();
+    // (2) x_hat, g1 and BCE of row q - 1 (rings: rows q-2, q-1, q)
+    if (i >= 2) {
+      const int r = q - 1;
+      const float* a0 = aring + ((i - 2) & 3) * NE_AROW;   // row q - 2
+      const float* a1 = aring + ((i - 1) & 3) * NE_AROW;   // row q - 1
+      const float* a2 = aring + (i & 3) * NE_AROW;         // row q
+      const bool inrow = r >= 0 && r < H, own = r >= r0 && r < r0 + TH;
+      float* gr = gring + (i & 3) * WP;                    // g1 row r0 - 3 + i
+#pragma unroll 2
+      for (int j = 0; j < 4; ++j) {
+        const int w = pl + 32 * j;
+        pkf2 s = pk2(0.f, 0.f);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float* ar = (t / 3 == 0) ? a0 : ((t / 3 == 1) ? a1 : a2);
+          const float4 av = ld4(ar + (w + t % 3) * C + c);
+          s = pkfma(pk2(av.x, av.y), wv2[0][t], s);
+          s = pkfma(pk2(av.z, av.w), wv2[1][t], s);
+        }
+        const float xh = ne_fold8(s.x + s.y) + bias;
+        float g = 0.f;
+        if (inrow) {
+          const float tgt = tcur[j];
+          g = cr * (ne_sigmoid(xh) - tgt);
+          if (own && cg == 0) {
+            x_hat[(size_t)b * HW + (size_t)r * W + w] = xh;
+            g1out[(size_t)b * HW + (size_t)r * W + w] = g;
+            bce += ne_bce(xh, tgt);
+            bsum += g;
+          }
+        }
+        if (cg == 0) gr[w + 1] = g;
+      }
+    }
+    load_tgt(q + 1, tcur);   // x_hat row q + 1 is computed at step i + 2
+    __syncthreads();
+    // (3) InstanceNorm-backward reduce + final-conv weight gradient of row q - 2
+    if (i >= 4) {
+      // g1 row r0 - 3 + i' is in slot i' & 3: rows q-1, q-2, q-3 were written at steps i,
+      // i-1, i-2
+      const float* gA = gring + ((i - 2) & 3) * WP;        // row q - 3
+      const float* gB = gring + ((i - 1) & 3) * WP;        // row q - 2
+      const float* gC = gring + (i & 3) * WP;              // row q - 1
+      const float* am = aring + ((i - 2) & 3) * NE_AROW;   // a of row q - 2
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int j = 0; j < 4; ++j) {
+        const int w = pl + 32 * j;
+        // nb[t] = g1[p - d(t)]: tap (kh, kw) reads row (q-2) + 1 - kh, column w + 1 - kw
+        float nb[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int kh = t / 3, kw = t % 3;
+          const float* grw = kh == 0 ? gC : (kh == 1 ? gB : gA);
+          nb[t] = grw[w + 2 - kw];
+        }
+        pkf2 ga[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          pkf2 sg = pk2(0.f, 0.f);
+#pragma unroll
+          for (int t = 0; t < 9; ++t) sg = pkfma(pk2(nb[t], nb[t]), wv2[k][t], sg);
+          ga[k] = sg;
+        }
+        const float4 a4 = ld4(am + (w + 1) * C + c);
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+        const float gav[4] = {ga[0].x, ga[0].y, ga[1].x, ga[1].y};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // xhat from a = lrelu(xhat): exact sign, |error| ~ 1 ulp on the negative side
+          const float xh = av[k] > 0.f ? av[k] : av[k] * (1.f / kSlope);
+          const float gx = gav[k] * slope(xh);
+          s1[k] += gx;
+          s2[k] = fmaf(gx, xh, s2[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const pkf2 f = pk2(av[2 * k], av[2 * k + 1]);
+#pragma unroll
+          for (int t = 0; t < 9; ++t) wacc2[k][t] = pkfma(pk2(nb[t], nb[t]), f, wacc2[k][t]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s1d[k] += (double)s1[k]; s2d[k] += (double)s2[k]; }
+    }
+  };
+#pragma unroll 1
+  for (int i = 0; i < TH + 4; i += 2) {
+    step(i, ybuf[0], tbuf[0]);
+    step(i + 1, ybuf[1], tbuf[1]);
+  }
+  __syncthreads();
+
+  // ---- band partials, fixed order: lanes of a channel group in-wave, then the 4 waves
+  const int lane = tid & 63, wave = tid >> 6;
+  double* red = reinterpret_cast<double*>(ne_sm);            // [2][4][NE_NTH]
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { red[(0 * 4 + k) * NE_NTH + tid] = s1d[k]; red[(1 * 4 + k) * NE_NTH + tid] = s2d[k]; }
+  __syncthreads();
+  const int slice = b * T + tile;
+  if (tid < 8) {   // channel group tid: sum over its 32 pixel lanes in order
+    double u[4] = {0.0, 0.0, 0.0, 0.0}, v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int p = 0; p < 32; ++p)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        u[k] += red[(0 * 4 + k) * NE_NTH + p * 8 + tid];
+        v[k] += red[(1 * 4 + k) * NE_NTH + p * 8 + tid];
+      }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) part[(size_t)slice * C + tid * 4 + k] = make_double2(u[k], v[k]);
+  }
+  __syncthreads();
+  // weight-gradient partials [slice][tap][0][ci]: fold the 32 pixel lanes of each channel group
+  float* wred = ne_sm;   // [4 waves][8 cg][36 + 2]
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float v = (k & 1) ? wacc2[k >> 1][t].y : wacc2[k >> 1][t].x;
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 8) wred[(wave * 8 + lane) * 38 + k * 9 + t] = v;
+    }
+  {
+    float v = bsum, e = bce;
+    v += __shfl_xor(v, 8, 64); v += __shfl_xor(v, 16, 64); v += __shfl_xor(v, 32, 64);
+    e += __shfl_xor(e, 8, 64); e += __shfl_xor(e, 16, 64); e += __shfl_xor(e, 32, 64);
+    if (lane == 0) { wred[(wave * 8) * 38 + 36] = v; wred[(wave * 8) * 38 + 37] = e; }
+  }
+  __syncthreads();
+  for (int i = tid; i < 8 * 36; i += NE_NTH) {
+    const int g = i / 36, e = i % 36, k = e / 9, t = e % 9;
+    const float s = wred[(0 * 8 + g) * 38 + e] + wred[(1 * 8 + g) * 38 + e] +
+                    wred[(2 * 8 + g) * 38 + e] + wred[(3 * 8 + g) * 38 + e];
+    wpart[((size_t)slice * 9 + t) * 32 + g * 4 + k] = s;
+  }
+  if (tid == 0) {
+    bpart[slice] = wred[0 * 38 + 36] + wred[8 * 38 + 36] + wred[16 * 38 + 36] + wred[24 * 38 + 36];
+    bce_part[slice] = wred[0 * 38 + 37] + wred[8 * 38 + 37] + wred[16 * 38 + 37] + wred[24 * 38 + 37];
+  }
+}
+
+}  // namespace ev
+
+using namespace ev;
+
+extern "C" int ebsdvae_net_end_tiles(int H, int W) {
+  return (W == NE_W && ev_dim_ok(H) && H % NE_TH == 0) ? H / NE_TH : -1;
+}
+
+extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float* w14, const float* b14,
+                               const float* x, const float* g_loss, float scale, float* x_hat,
+                               float* g1, float* bce_part, double* part, float* wpart, float* bpart,
+                               int B, int H, int W, int C, ebsdvae_stream_t stream) {
+  EV_REQUIRE(y13 && st13 && w14 && x && x_hat && g1 && bce_part && part && wpart && bpart && B > 0,
+             "net_end: null pointer");
+  EV_REQUIRE(C == NE_C && ebsdvae_net_end_tiles(H, W) > 0,
+             "net_end: C=%d %dx%d unsupported (C 32, W %d, H a multiple of %d)", C, H, W, NE_W, NE_TH);
+  const int T = H / NE_TH;
+  const float gscale = scale / ((float)B * (float)(H * W));
+  const size_t lds = (size_t)(NE_RING * NE_AROW + NE_RING * NE_WP) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)net_end_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    once = true;
+  }
+  hipLaunchKernelGGL(net_end_kernel, dim3(T, B), dim3(NE_NTH), lds, (hipStream_t)stream, y13,
+                     (const float2*)st13, w14, b14, x, g_loss, gscale, x_hat, g1, bce_part,
+                     (double2*)part, wpart, bpart, H);
+  return evh::check_launch("net_end");
+}

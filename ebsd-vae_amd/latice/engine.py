@@ -729,6 +729,64 @@ def in_backward_final(g1, w14, y, st, dw14, db14):
     return gy
 
 
+# ----------------------------------------------------------------------------- network end
+# ebsdvae_net_end: the final conv's forward, the BCE part of the loss and its logit gradient, and
+# the last block's InstanceNorm-backward reduce + the final conv's gradient slices in one pass
+# over y13 (the training step).  Off by default until it times faster than the separate
+# kernels it replaces (EBSDVAE_NET_END=1 turns it on).
+_NET_END = os.environ.get("EBSDVAE_NET_END", "0") != "0"
+
+
+@dataclass
+class NetEnd:
+    g1: torch.Tensor      # (B, S, S) logit gradient of the mean BCE
+    part: torch.Tensor    # (B, T, C, 2) float64 reduce sums of the last block
+    wpart: torch.Tensor   # (B*T, 9, 1, C) final-conv weight-gradient slices
+    bpart: torch.Tensor   # (B*T,)
+    bce: torch.Tensor     # (B, T) per-band BCE sums
+    tiles: int
+
+
+def net_end_ok(plan: Plan) -> bool:
+    S = plan.image_size
+    return _NET_END and plan.inplanes == 32 and N.call("ebsdvae_net_end_tiles", S, S) > 0
+
+
+def network_end(plan: Plan, saved, params, x, g_loss=None, scale: float = 1.0):
+    """x_hat and a NetEnd from the decoder's saved last block (decoder_forward(final=False))."""
+    y13, st13 = saved[plan.dec[-1].name]
+    B, H, W, C = y13.shape
+    T = N.call("ebsdvae_net_end_tiles", H, W)
+    x_hat = _empty(B, 1, H, W, like=y13)
+    g1 = _empty(B, H, W, like=y13)
+    bce = _empty(B, T, like=y13)
+    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y13.device)
+    wpart = _empty(B * T, 9, 1, C, like=y13)
+    bpart = _empty(B * T, like=y13)
+    N.call("ebsdvae_net_end", N.ptr(y13), N.ptr(st13), N.ptr(params["decoder.14.weight"]),
+           N.ptr(params["decoder.14.bias"]), N.ptr(x), N.ptr(g_loss), float(scale), N.ptr(x_hat),
+           N.ptr(g1), N.ptr(bce), part.data_ptr(), N.ptr(wpart), N.ptr(bpart), B, H, W, C,
+           N.stream())
+    return x_hat, NetEnd(g1, part, wpart, bpart, bce, T)
+
+
+def in_backward_final_from(end: NetEnd, w14, y, st, dw14, db14):
+    """in_backward_final with the reduce pass already done by network_end."""
+    B, H, W, C = y.shape
+    bst = _in_bwd_stats(B, C, end.tiles, H * W, end.part, y)
+    gy = torch.empty_like(y)
+    if _FWD_PIECES.get(_PRECISION):
+        gmax = _empty(B, N.call("ebsdvae_in_bwd_final_tiles", H, W), like=y)
+        N.call("ebsdvae_in_bwd_final_apply_max", N.ptr(end.g1), N.ptr(w14), N.ptr(y), N.ptr(st),
+               N.ptr(bst), N.ptr(gy), N.ptr(gmax), B, H, W, C, N.stream())
+        gy.ev_gmax = gmax
+    else:
+        N.call("ebsdvae_in_bwd_final_apply", N.ptr(end.g1), N.ptr(w14), N.ptr(y), N.ptr(st), N.ptr(bst),
+               N.ptr(gy), B, H, W, C, N.stream())
+    _reduce_slices(end.wpart, end.bpart, B * end.tiles, C, 1, KIND_CONV, dw14, db14)
+    return gy
+
+
 def in_backward_first(gnext, y, st, x, dw0, db0, part=None, w0=None, b0=None):
     """Backward of the first conv block (latice/model.py:110): writes dW/db of the 1->32
     conv directly from the InstanceNorm-backward apply pass (gy is never materialised).
@@ -1059,8 +1117,9 @@ def heads_backward(plan: Plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, param
 
 
 # ----------------------------------------------------------------------------- decoder
-def decoder_forward(plan: Plan, dec_in, params, packs=None):
-    """dec_in: (B,s,s,C) NHWC.  Returns (x_hat (B,1,S,S), saved)."""
+def decoder_forward(plan: Plan, dec_in, params, packs=None, final=True):
+    """dec_in: (B,s,s,C) NHWC.  Returns (x_hat (B,1,S,S), saved).  final=False leaves out the
+    final conv (x_hat None): the training step computes it in network_end."""
     B = dec_in.shape[0]
     saved = {"__dec_in__": dec_in}
     src, sst = dec_in, None
@@ -1070,6 +1129,8 @@ def decoder_forward(plan: Plan, dec_in, params, packs=None):
         saved[L.name] = (y, st)
         src, sst = y, st
     _record(plan.dec, saved)
+    if not final:
+        return None, saved
     S = plan.image_size
     x_hat = _empty(B, 1, S, S, like=dec_in)
     N.call("ebsdvae_conv3x3_cout1_fwd", N.ptr(src), N.ptr(sst), ACT_NORM,
@@ -1078,26 +1139,31 @@ def decoder_forward(plan: Plan, dec_in, params, packs=None):
     return x_hat, saved
 
 
-def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None, packs=None):
+def decoder_backward(plan: Plan, g_xhat, saved, params, grads=None, packs=None, end=None):
     """g_xhat: (B,1,S,S).  Returns (grads dict, g_dec_in (B,s,s,C) NHWC).  The layers'
-    weight-gradient reductions run batched when it returns."""
+    weight-gradient reductions run batched when it returns.  end: the NetEnd of network_end
+    (g_xhat None), whose pass already produced the last block's reduce sums and the final
+    conv's gradient slices."""
     with batched_wgrad_reduce():
-        return _decoder_backward(plan, g_xhat, saved, params, grads, packs)
+        return _decoder_backward(plan, g_xhat, saved, params, grads, packs, end)
 
 
-def _decoder_backward(plan, g_xhat, saved, params, grads, packs):
+def _decoder_backward(plan, g_xhat, saved, params, grads, packs, end=None):
     out = {}
-    B = g_xhat.shape[0]
-    S, p = plan.image_size, plan.inplanes
     last = plan.dec[-1]
     y13, st13 = saved[last.name]
+    B = y13.shape[0]
+    S, p = plan.image_size, plan.inplanes
     wn, bn = "decoder.14.weight", "decoder.14.bias"
     dw = _grad_buf(grads, wn, params[wn])
     db = _grad_buf(grads, bn, params[bn])
-    g1 = g_xhat.reshape(B, S, S)
-    # last conv fused into the last block's InstanceNorm backward: its input gradient is
-    # recomputed from g1 on the fly, its weight gradient accumulated in the reduce pass
-    gy_last = in_backward_final(g1, params[wn], y13, st13, dw, db)
+    if end is not None:
+        gy_last = in_backward_final_from(end, params[wn], y13, st13, dw, db)
+    else:
+        g1 = g_xhat.reshape(B, S, S)
+        # last conv fused into the last block's InstanceNorm backward: its input gradient is
+        # recomputed from g1 on the fly, its weight gradient accumulated in the reduce pass
+        gy_last = in_backward_final(g1, params[wn], y13, st13, dw, db)
     out[wn], out[bn] = dw, db
     g_next, part = None, None
     for i in reversed(range(len(plan.dec))):
@@ -1121,7 +1187,7 @@ def _decoder_backward(plan, g_xhat, saved, params, grads, packs):
         else:
             g_next = conv_dgrad(gy, L, params[wn], wd=_wp(packs, L.name, 1))
     s, C = plan.enc_side, plan.enc_channels
-    g_dec = _empty(B, s, s, C, like=g_xhat)
+    g_dec = _empty(B, s, s, C, like=y13)
     N.call("ebsdvae_upsample2_bwd", N.ptr(g_next), N.ptr(g_dec), B, s, s, C, N.stream())
     return out, g_dec
 
@@ -1152,8 +1218,35 @@ def loss_forward(x_hat, x, z, mu, std, kl_lambda: float):
     return (loss, kl_loss, recon_loss), (elbo, kl, recon)
 
 
+def loss_forward_parts(end: NetEnd, z, mu, std, kl_lambda: float, P: int):
+    """loss_forward with the BCE sums of network_end (same outputs, same side-stream rule)."""
+    B, L = z.shape
+    elbo, kl, recon = _empty(B, like=z), _empty(B, like=z), _empty(B, like=z)
+    loss, kl_loss, recon_loss = (torch.empty((), dtype=torch.float32, device=z.device)
+                                 for _ in range(3))
+    side = _side_stream(z.device) if _DEFER else None
+    ctx = contextlib.nullcontext()
+    if side is not None:
+        side = _side_use(z.device, end.bce, z, mu, std, elbo, kl, recon, loss, kl_loss, recon_loss)
+        ctx = torch.cuda.stream(side)
+    with ctx:
+        N.call("ebsdvae_vae_loss_fwd_parts", N.ptr(end.bce), end.tiles, N.ptr(z), N.ptr(mu),
+               N.ptr(std), float(kl_lambda), N.ptr(elbo), N.ptr(kl), N.ptr(recon), N.ptr(loss),
+               N.ptr(kl_loss), N.ptr(recon_loss), B, P, L, N.stream())
+    return (loss, kl_loss, recon_loss), (elbo, kl, recon)
+
+
 def loss_backward(x_hat, x, z, mu, std, kl_lambda: float, g_loss=None, g_kl=None, g_recon=None,
-                  g_elbo=None, scale: float = 1.0, need_gx=False, out=None):
+                  g_elbo=None, scale: float = 1.0, need_gx=False, out=None, P: int | None = None):
+    """x_hat None (with P the pixels per pattern): only the KL gradients (network_end made the
+    logit gradient); g_xhat is then None."""
+    if x_hat is None:
+        B, L = z.shape
+        g_z, g_mu, g_std = torch.empty_like(z), torch.empty_like(mu), torch.empty_like(std)
+        N.call("ebsdvae_vae_loss_bwd", None, None, N.ptr(z), N.ptr(mu), N.ptr(std),
+               float(kl_lambda), N.ptr(g_loss), N.ptr(g_kl), N.ptr(g_recon), N.ptr(g_elbo),
+               float(scale), None, N.ptr(g_z), N.ptr(g_mu), N.ptr(g_std), None, B, P, L, N.stream())
+        return None, g_z, g_mu, g_std, None
     """Gradients of the loss outputs w.r.t. (x_hat, z, mu, std[, x]).  `out` may supply the
     four destination tensors (persistent buffers for graph capture)."""
     B = x_hat.shape[0]

@@ -143,15 +143,27 @@ class VAETrainer:
             ready = None
         enc, se = E.encoder_forward(plan, x, P, packs=packs, packs_ready=ready)
         flat, mu, std, z, dec_in = E.heads_forward(plan, enc, P, eps)
-        x_hat, sd = E.decoder_forward(plan, dec_in, P, packs=packs)
+        fused_end = E.net_end_ok(plan)
+        x_hat, sd = E.decoder_forward(plan, dec_in, P, packs=packs, final=not fused_end)
         # the side stream (weight gradients, their slice reductions, the heads' weight
         # gradients, the loss values) is joined once, after the encoder backward: only the
         # chain loss backward -> input gradients -> ... stays on the current stream
         with E.deferred_side_join(x.device):
-            (loss, kl, rec), _ = E.loss_forward(x_hat, x, z, mu, std, self.kl_lambda)
-            g_xhat, g_z, g_mu, g_std, _ = E.loss_backward(x_hat, x, z, mu, std, self.kl_lambda,
-                                                          g_loss=self.one, scale=1.0 / self.world)
-            _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
+            if fused_end:
+                # final conv + BCE + its logit gradient + the last block's reduce: one pass
+                x_hat, end = E.network_end(plan, sd, P, x, g_loss=self.one, scale=1.0 / self.world)
+                (loss, kl, rec), _ = E.loss_forward_parts(end, z, mu, std, self.kl_lambda,
+                                                          x[0].numel())
+                _, g_z, g_mu, g_std, _ = E.loss_backward(None, None, z, mu, std, self.kl_lambda,
+                                                         g_loss=self.one, scale=1.0 / self.world,
+                                                         P=x[0].numel())
+                _, g_dec = E.decoder_backward(plan, None, sd, P, grads=G, packs=packs, end=end)
+            else:
+                (loss, kl, rec), _ = E.loss_forward(x_hat, x, z, mu, std, self.kl_lambda)
+                g_xhat, g_z, g_mu, g_std, _ = E.loss_backward(x_hat, x, z, mu, std, self.kl_lambda,
+                                                              g_loss=self.one,
+                                                              scale=1.0 / self.world)
+                _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
             g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P,
                                         grads=G)
             if self.reducer.active:

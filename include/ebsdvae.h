@@ -365,13 +365,43 @@ int ebsdvae_vae_loss_fwd(const float* x_hat, const float* x, const float* z, con
                          int P, int L, ebsdvae_stream_t stream);
 /* upstream gradients g_loss, g_kl_loss, g_recon_loss (device scalars) and g_elbo (B) may
  * each be NULL (= 0); scale multiplies all of them (e.g. 1/world_size for data
- * parallelism).  g_x (gradient w.r.t. the BCE target) may be NULL. */
+ * parallelism).  g_x (gradient w.r.t. the BCE target) may be NULL.  g_xhat may be NULL (then
+ * x_hat and x may be too): only the KL gradients g_z, g_mu, g_std are written (the training
+ * step's logit gradient comes from ebsdvae_net_end). */
 int ebsdvae_vae_loss_bwd(const float* x_hat, const float* x, const float* z, const float* mu,
                          const float* std, float kl_lambda, const float* g_loss,
                          const float* g_kl_loss, const float* g_recon_loss,
                          const float* g_elbo, float scale, float* g_xhat, float* g_z,
                          float* g_mu, float* g_std, float* g_x, int B, int P, int L,
                          ebsdvae_stream_t stream);
+
+/* As ebsdvae_vae_loss_fwd with recon_b = sum_t bce_part[b][t] / P from the per-row-band BCE
+ * sums of ebsdvae_net_end (tiles = ebsdvae_net_end_tiles(H, W)). */
+int ebsdvae_vae_loss_fwd_parts(const float* bce_part, int tiles, const float* z, const float* mu,
+                               const float* std, float kl_lambda, float* elbo, float* kl,
+                               float* recon, float* loss, float* kl_loss, float* recon_loss, int B,
+                               int P, int L, ebsdvae_stream_t stream);
+
+/* ---- network end of the training step (latice/model.py:147-148 + lightning_module.py:79-92) --
+ * One pass over the last block's pre-norm output y13 (B, H, W, C) NHWC with its statistics
+ * st13 {mean, rstd} (B, C), for C == 32, W == 128, H % 16 == 0:
+ *   x_hat (B, 1, H, W) = Conv2d(32, 1)(lrelu(IN(y13))) with w14 (1, 32, 3, 3), b14 (1) or NULL;
+ *   g1 (B, H, W) = g_loss * scale / (B * H * W) * (sigmoid(x_hat) - x), the gradient of the
+ *     mean-BCE part of the loss w.r.t. the logits (g_loss a device scalar, NULL = 1);
+ *   bce_part (B, T): per row band the sum of BCE-with-logits(x_hat, x);
+ *   part (B, T, C) double2: the InstanceNorm-backward reduce sums of the last block with its
+ *     output gradient recomputed from g1 (as ebsdvae_in_bwd_final_reduce; finalize with
+ *     ebsdvae_in_bwd_finalize(part, ..., T, H * W));
+ *   wpart (B * T, 9, 1, C) / bpart (B * T): the final conv's weight / bias gradient slices for
+ *     ebsdvae_wgrad_reduce (cin C, cout 1, kind 0).
+ * T = ebsdvae_net_end_tiles(H, W) (-1: shape unsupported).  Replaces ebsdvae_conv3x3_cout1_fwd,
+ * the BCE part of ebsdvae_vae_loss_fwd / _bwd and ebsdvae_in_bwd_final_reduce, which read y13
+ * once each. */
+int ebsdvae_net_end_tiles(int H, int W);
+int ebsdvae_net_end(const float* y13, const float* st13, const float* w14, const float* b14,
+                    const float* x, const float* g_loss, float scale, float* x_hat, float* g1,
+                    float* bce_part, double* part, float* wpart, float* bpart, int B, int H, int W,
+                    int C, ebsdvae_stream_t stream);
 
 /* ---- optimiser (torch.optim.Adam semantics; latice/lightning_module.py:26-28) ---------
  * state: device float step counter (incremented by this call), m, v, vmax (amsgrad). */

@@ -112,6 +112,13 @@ int main() {
   expect_err(ebsdvae_ingest_patterns(nullptr, 7, 2, 140, 140, 128, 128, nullptr, nullptr),
              "ingest dtype");
   expect_err(ebsdvae_normal_fill(nullptr, 16, 1, 0, nullptr, nullptr), "normal null");
+  for (int H : sizes) acc += ebsdvae_net_end_tiles(H, 128) + ebsdvae_net_end_tiles(H, H);
+  expect_err(ebsdvae_net_end(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1.f, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr, 2, 128, 128, 32, nullptr),
+             "net_end null");
+  expect_err(ebsdvae_vae_loss_fwd_parts(nullptr, 8, nullptr, nullptr, nullptr, 0.f, nullptr, nullptr,
+                                        nullptr, nullptr, nullptr, nullptr, 2, 16384, 16, nullptr),
+             "loss_fwd_parts null");
   printf("abi_asan: %s (query checksum %lld)\n", g_fail ? "FAILED" : "ok", acc);
   return g_fail ? 1 : 0;
 }

@@ -908,3 +908,60 @@ def test_fused_bwd_finalize_bitwise(cuda, B, H, cin, cout, pmode):
     torch.cuda.synchronize()
     for a, b_ in zip(*outs):
         assert torch.equal(a, b_)
+
+
+def test_network_end_matches_oracle(cuda):
+    """ebsdvae_net_end (the training step's network end in one pass over y13): x_hat of the final
+    conv, the mean-BCE logit gradient g1, the per-band BCE sums, the last block's
+    InstanceNorm-backward reduce (finalized here) and the final conv's gradient slices, against
+    the float64 oracle; then the apply pass it feeds gives the block's output gradient."""
+    rng = np.random.default_rng(33)
+    B, H, C = 3, 128, 32
+    y = rng.standard_normal((B, H, H, C)) * 1.3 - 0.4
+    xh, mean, rstd = O.instance_norm(y)
+    st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)
+    w14 = rng.standard_normal((1, C, 3, 3)) * 0.15
+    b14 = np.array([0.07])
+    x = np.floor(rng.random((B, 1, H, H)) * 255) / 255
+    scale = 0.5
+    P = H * H
+    T = N.call("ebsdvae_net_end_tiles", H, H)
+    assert T == H // 16
+    plan = E.build_plan()
+    params = {"decoder.14.weight": dev(w14), "decoder.14.bias": dev(b14)}
+    saved = {plan.dec[-1].name: (dev(y), dev(st))}
+    g_loss = torch.ones((), device="cuda")
+    x_hat, end = E.network_end(plan, saved, params, dev(x), g_loss=g_loss, scale=scale)
+    a = O.lrelu(xh)
+    ref_xhat = O.conv3x3(a, w14, b14)[..., 0]                     # (B, H, H)
+    sig = 1.0 / (1.0 + np.exp(-ref_xhat))
+    ref_g1 = scale / (B * P) * (sig - x[:, 0])
+    bce = (1 - x[:, 0]) * ref_xhat + np.maximum(-ref_xhat, 0) + np.log1p(np.exp(-np.abs(ref_xhat)))
+    assert O.rel_err(host(x_hat)[:, 0], ref_xhat) < 2e-5
+    assert O.rel_err(host(end.g1), ref_g1) < 2e-5
+    ref_bce = bce.reshape(B, T, -1).sum(-1)
+    assert O.rel_err(host(end.bce), ref_bce) < 1e-5
+    # reduce sums of the last block, finalized, and the apply that consumes them
+    ga = O.conv3x3_dgrad(ref_g1[..., None], w14)
+    gxs = ga * O.lrelu_slope(xh)
+    s1 = gxs.reshape(B, T, -1, C).sum(2)
+    s2 = (gxs * xh).reshape(B, T, -1, C).sum(2)
+    part = host(end.part)
+    assert O.rel_err(part[..., 0], s1) < 1e-4 and O.rel_err(part[..., 1], s2) < 1e-4
+    dw = torch.empty(1, C, 3, 3, device="cuda")
+    db = torch.empty(1, device="cuda")
+    gy = E.in_backward_final_from(end, dev(w14), dev(y), dev(st), dw, db)
+    ref_gy = O.instance_norm_bwd(gxs, xh, rstd)
+    rw, rb = O.conv3x3_wgrad(a, ref_g1[..., None])
+    print(f"\nnet_end: gy {O.rel_err(host(gy), ref_gy):.2e} dW14 {O.rel_err(host(dw), rw):.2e} "
+          f"db14 {O.rel_err(host(db), rb):.2e}")
+    assert O.rel_err(host(gy), ref_gy) < 1e-4
+    assert O.rel_err(host(dw), rw) < 5e-5
+    assert O.rel_err(host(db), rb) < 5e-5
+    # the loss values from the band sums
+    z = rng.standard_normal((B, 16)); mu = rng.standard_normal((B, 16)) * 0.3
+    sd = np.exp(rng.standard_normal((B, 16)) * 0.2)
+    (loss, klm, recm), (elbo, kl, rec) = E.loss_forward_parts(end, dev(z), dev(mu), dev(sd), 5e-6, P)
+    ref = O.vae_loss(ref_xhat[:, None], x, z, mu, sd, 5e-6)
+    assert abs(float(loss) - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    assert O.rel_err(host(elbo), ref["elbo"]) < 1e-5

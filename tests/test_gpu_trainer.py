@@ -90,3 +90,30 @@ def test_trainer_full_size_gradient_batch_independence(cuda):
     err = float((g_full - g_mean).abs().max() / g_mean.abs().max())
     print(f"\nfull-batch gradient vs mean of halves: {err:.2e}")
     assert np.isfinite(err) and err < 1e-4
+
+
+@pytest.mark.parametrize("prec", ["f16x3", "fp32"])
+def test_trainer_network_end_fusion_matches_separate_kernels(cuda, prec, monkeypatch):
+    """The fused network end (ebsdvae_net_end) and the separate final conv / loss / reduce
+    kernels give the same step: loss scalars and every gradient within fp32 reordering."""
+    from latice.seeding import seeded_eps, seeded_state_dict, synthetic_patterns
+    sd = {k: torch.from_numpy(v) for k, v in seeded_state_dict(0).items()}
+    x = torch.from_numpy(synthetic_patterns(4, 16)).to(cuda)
+    eps = torch.from_numpy(seeded_eps(4, 16)).to(cuda)
+    out = {}
+    with E.precision(prec):
+        for fused in (True, False):
+            monkeypatch.setattr(E, "_NET_END", fused)
+            m = VariationalAutoEncoderRawData().to(cuda)
+            m.load_state_dict(sd)
+            tr = VAETrainer(m, kl_lambda=5e-6)
+            assert E.net_end_ok(m.plan) == fused   # 128x128: the fused kernel's shape
+            loss, kl, rec = tr.forward_backward(x, eps)
+            torch.cuda.synchronize()
+            out[fused] = ([float(loss), float(kl), float(rec)], tr.gflat.clone(), dict(tr.G))
+    (l1, g1, G1), (l0, g0, G0) = out[True], out[False]
+    for a, b in zip(l1, l0):
+        assert abs(a - b) <= 1e-6 * abs(b) + 1e-12
+    worst = max(O.rel_err(host(G1[n]), host(G0[n])) for n in G1 if n.endswith("weight"))
+    print(f"\n[{prec}] fused vs separate network end: worst weight-grad rel err {worst:.2e}")
+    assert worst < 1e-4

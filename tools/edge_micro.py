@@ -46,7 +46,26 @@ def main():
     yc = torch.empty(B, H, H, C, device=dev)
     spart = torch.empty(B, N.call("ebsdvae_conv3x3_stat_tiles", H, H, C), C, 2, device=dev)
     E4 = B * H * H * C * 4
+    Tn = N.call("ebsdvae_net_end_tiles", H, H)
+    ne_out = [torch.empty(B, H, H, device=dev) for _ in range(2)]
+    ne_bce = torch.empty(B, max(Tn, 1), device=dev)
+    ne_part = torch.empty(B, max(Tn, 1), C, 2, dtype=torch.float64, device=dev)
+    ne_w = torch.empty(B * max(Tn, 1), 9, C, device=dev)
+    ne_b = torch.empty(B * max(Tn, 1), device=dev)
+    one = torch.ones((), device=dev)
+    w0 = torch.randn(C, 1, 3, 3, device=dev, generator=g) * 0.3
+    Tf = N.call("ebsdvae_conv_first_stat_tiles", H, H)
+    fpart = torch.empty(B, Tf, C, 2, device=dev)
     cases = {
+        "first_valu": (lambda: N.call("ebsdvae_conv_first_fwd", N.ptr(x), N.ptr(w0), N.ptr(b), N.ptr(yc),
+                                      N.ptr(fpart), B, H, H, C, s), E4 + E4 // 32),
+        "first_rc": (lambda: N.call("ebsdvae_in_bwd_first_apply_wgrad_rc", N.ptr(y2), N.ptr(w0), N.ptr(b),
+                                    N.ptr(st), N.ptr(bst), N.ptr(x), N.ptr(wpart), N.ptr(bpart),
+                                    B, H, H, C, s), E4 + E4 // 32),
+        "net_end": (lambda: N.call("ebsdvae_net_end", N.ptr(y), N.ptr(st), N.ptr(w14), N.ptr(b), N.ptr(x),
+                                   N.ptr(one), 1.0, N.ptr(ne_out[0]), N.ptr(ne_out[1]), N.ptr(ne_bce),
+                                   ne_part.data_ptr(), N.ptr(ne_w), N.ptr(ne_b), B, H, H, C, s),
+                    E4 + 3 * E4 // 32),
         # name: (launch, algorithmic bytes)
         "small1": (lambda: N.call("ebsdvae_conv3x3_fwd", N.ptr(x), None, ACT_RAW, N.ptr(w1), N.ptr(b),
                                   N.ptr(yc), N.ptr(spart), None, B, H, H, 1, C, s), E4 + E4 // 32),
