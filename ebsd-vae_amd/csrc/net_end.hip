@@ -101,23 +101,22 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
   for (int k = 0; k < 2; ++k)
 #pragma unroll
     for (int t = 0; t < 9; ++t) wacc2[k][t] = pk2(0.f, 0.f);
-  float bsum = 0.f, bce = 0.f;   // g1 and BCE sums over the band (cg == 0 lanes)
+  float bsum = 0.f, bce = 0.f;   // g1 and BCE sums over the band (lanes cg < 4)
 
-  // the BCE target of x_hat row r0 - 3 + i, loaded two steps ahead (its pixels pl + 32 j)
-  auto load_tgt = [&](int r, float (&d)[4]) EV_LAMBDA_INLINE {
-    const bool in = r >= 0 && r < H;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] = in ? xt[(size_t)b * HW + (size_t)r * W + pl + 32 * j] : 0.f;
+  // the BCE target of x_hat row r0 - 3 + i, loaded two steps ahead: lanes cg < 4 own pixel
+  // pl + 32 cg of the row for the logit-gradient / BCE work (one evaluation per pixel)
+  auto load_tgt = [&](int r, float& d) EV_LAMBDA_INLINE {
+    d = (r >= 0 && r < H && cg < 4) ? xt[(size_t)b * HW + (size_t)r * W + pl + 32 * cg] : 0.f;
   };
   float4 ybuf[2][4];
-  float tbuf[2][4];
+  float tbuf[2];
   load_row(r0 - 2, ybuf[0]);
   load_row(r0 - 1, ybuf[1]);
   load_tgt(r0 - 3, tbuf[0]);
   load_tgt(r0 - 2, tbuf[1]);
   __syncthreads();   // ring columns zeroed
 
-  auto step = [&](int i, float4 (&ycur)[4], float (&tcur)[4]) EV_LAMBDA_INLINE {
+  auto step = [&](int i, float4 (&ycur)[4], float& tcur) EV_LAMBDA_INLINE {
     const int q = r0 - 2 + i;
     // (1) a = lrelu(IN(y13)) of source row q into ring slot i & 3 (zero outside the image)
     {
@@ -143,6 +142,7 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
       const float* a2 = aring + (i & 3) * NE_AROW;         // row q
       const bool inrow = r >= 0 && r < H, own = r >= r0 && r < r0 + TH;
       float* gr = gring + (i & 3) * WP;                    // g1 row r0 - 3 + i
+      float xsel = 0.f;   // x_hat of pixel pl + 32 cg (lanes cg < 4)
 #pragma unroll 2
       for (int j = 0; j < 4; ++j) {
         const int w = pl + 32 * j;
@@ -155,18 +155,21 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
           s = pkfma(pk2(av.z, av.w), wv2[1][t], s);
         }
         const float xh = ne_fold8(s.x + s.y) + bias;
+        xsel = cg == j ? xh : xsel;
+      }
+      if (cg < 4) {
+        const int w = pl + 32 * cg;
         float g = 0.f;
         if (inrow) {
-          const float tgt = tcur[j];
-          g = cr * (ne_sigmoid(xh) - tgt);
-          if (own && cg == 0) {
-            x_hat[(size_t)b * HW + (size_t)r * W + w] = xh;
+          g = cr * (ne_sigmoid(xsel) - tcur);
+          if (own) {
+            x_hat[(size_t)b * HW + (size_t)r * W + w] = xsel;
             g1out[(size_t)b * HW + (size_t)r * W + w] = g;
-            bce += ne_bce(xh, tgt);
+            bce += ne_bce(xsel, tcur);
             bsum += g;
           }
         }
-        if (cg == 0) gr[w + 1] = g;
+        gr[w + 1] = g;
       }
     }
     load_tgt(q + 1, tcur);   // x_hat row q + 1 is computed at step i + 2
@@ -260,9 +263,9 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
       if (lane < 8) wred[(wave * 8 + lane) * 38 + k * 9 + t] = v;
     }
   {
-    float v = bsum, e = bce;
-    v += __shfl_xor(v, 8, 64); v += __shfl_xor(v, 16, 64); v += __shfl_xor(v, 32, 64);
-    e += __shfl_xor(e, 8, 64); e += __shfl_xor(e, 16, 64); e += __shfl_xor(e, 32, 64);
+    float v = bsum, e = bce;   // lanes cg < 4 hold pixel sums: fold over all 64 lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { v += __shfl_xor(v, o, 64); e += __shfl_xor(e, o, 64); }
     if (lane == 0) { wred[(wave * 8) * 38 + 36] = v; wred[(wave * 8) * 38 + 37] = e; }
   }
   __syncthreads();

@@ -732,9 +732,8 @@ def in_backward_final(g1, w14, y, st, dw14, db14):
 # ----------------------------------------------------------------------------- network end
 # ebsdvae_net_end: the final conv's forward, the BCE part of the loss and its logit gradient, and
 # the last block's InstanceNorm-backward reduce + the final conv's gradient slices in one pass
-# over y13 (the training step).  Off by default until it times faster than the separate
-# kernels it replaces (EBSDVAE_NET_END=1 turns it on).
-_NET_END = os.environ.get("EBSDVAE_NET_END", "0") != "0"
+# over y13 (the training step; EBSDVAE_NET_END=0 keeps the separate kernels for A/B timing).
+_NET_END = os.environ.get("EBSDVAE_NET_END", "1") != "0"
 
 
 @dataclass
