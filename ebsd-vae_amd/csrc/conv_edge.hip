@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w0, const float* __restrict__ b0,
     float* __restrict__ y, float2* __restrict__ part, int H, int W, int TH) {
   extern __shared__ float xs[];   // (TH + 2) x (W + 2)
-  __shared__ float red[8][32][4];
+  __shared__ float red[8][8][4];   // [wave (mean) | 4 + wave (M2)][channel group][k]
   const int tile = blockIdx.x, b = blockIdx.y, T = gridDim.x;
   const int tid = threadIdx.x, cg = tid & 7, pr = tid >> 3;
   const int c = cg * 4, r0 = tile * TH, WP = W + 2;
@@ -281,17 +281,23 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
     }
     st4(yb + (size_t)p * FIRST_C, make_float4(v[j][0], v[j][1], v[j][2], v[j][3]));
   }
-  // band statistics per channel, fixed order: 32 pixel lanes folded through LDS
+  // band statistics per channel, fixed order: the 8 pixel lanes of a wave by a shuffle tree
+  // (lanes cg, cg + 8, ..., cg + 56), then the 4 waves through LDS (a serial walk over 32
+  // LDS partials per channel cost ~8 us per block)
+  const int lane = tid & 63, wave = tid >> 6;
   float mean[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) red[cg][pr][k] = s[k];
+  for (int k = 0; k < 4; ++k) {
+    float a = s[k];
+    a += __shfl_xor(a, 8, 64);
+    a += __shfl_xor(a, 16, 64);
+    a += __shfl_xor(a, 32, 64);
+    if (lane < 8) red[wave][lane][k] = a;
+  }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float a = 0.f;
-    for (int i = 0; i < 32; ++i) a += red[cg][i][k];
-    mean[k] = a * (1.0f / FIRST_PX);
-  }
+  for (int k = 0; k < 4; ++k)
+    mean[k] = (red[0][cg][k] + red[1][cg][k] + red[2][cg][k] + red[3][cg][k]) * (1.0f / FIRST_PX);
   float q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < FIRST_NPT; ++j)
@@ -300,17 +306,20 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
       const float d = v[j][k] - mean[k];
       q[k] = fmaf(d, d, q[k]);
     }
-  __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) red[cg][pr][k] = q[k];
+  for (int k = 0; k < 4; ++k) {
+    float a = q[k];
+    a += __shfl_xor(a, 8, 64);
+    a += __shfl_xor(a, 16, 64);
+    a += __shfl_xor(a, 32, 64);
+    if (lane < 8) red[4 + wave][lane][k] = a;
+  }
   __syncthreads();
-  if (pr == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float a = 0.f;
-      for (int i = 0; i < 32; ++i) a += red[cg][i][k];
-      part[((size_t)b * T + tile) * FIRST_C + c + k] = make_float2(mean[k], a);
-    }
+  if (tid < FIRST_C) {   // channel tid: group tid / 4, element tid % 4
+    const int g = tid >> 2, k = tid & 3;
+    const float m = (red[0][g][k] + red[1][g][k] + red[2][g][k] + red[3][g][k]) * (1.0f / FIRST_PX);
+    part[((size_t)b * T + tile) * FIRST_C + tid] =
+        make_float2(m, red[4][g][k] + red[5][g][k] + red[6][g][k] + red[7][g][k]);
   }
 }
 

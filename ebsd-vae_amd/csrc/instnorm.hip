@@ -427,21 +427,22 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     __syncthreads();
     if (tid == 0) gmax[slice] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
   }
-  if (!APPLY) {   // InstanceNorm-backward plane partials (double, fixed order)
+  if (!APPLY) {   // InstanceNorm-backward plane partials (double, fixed order): the pixel
+                  // lanes of a wave by a shuffle tree, then the 4 waves through LDS
+    double* rd = &red[0][0][0];   // [4 waves][C][2]
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { red[0][k][tid] = a1[k]; red[1][k][tid] = a2[k]; }
+    for (int k = 0; k < 4; ++k) {
+      double u = a1[k], v = a2[k];
+#pragma unroll
+      for (int o = CG; o < 64; o <<= 1) { u += __shfl_xor(u, o, 64); v += __shfl_xor(v, o, 64); }
+      if (lane < CG) { rd[(wave * C + lane * 4 + k) * 2] = u; rd[(wave * C + lane * 4 + k) * 2 + 1] = v; }
+    }
     __syncthreads();
-    if (tid < CG) {
-      double u[4], v[4];
+    if (tid < C) {
+      double u = 0.0, v = 0.0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { u[k] = red[0][k][tid]; v[k] = red[1][k][tid]; }
-      for (int r = 1; r < NPR; ++r) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { u[k] += red[0][k][r * CG + tid]; v[k] += red[1][k][r * CG + tid]; }
-      }
-      double2* op = part + (size_t)slice * C + c;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) op[k] = make_double2(u[k], v[k]);
+      for (int wv = 0; wv < 4; ++wv) { u += rd[(wv * C + tid) * 2]; v += rd[(wv * C + tid) * 2 + 1]; }
+      part[(size_t)slice * C + tid] = make_double2(u, v);
     }
   }
   if ((FUSE_ == FUSE_FINAL && !APPLY) || (FUSE_ == FUSE_FIRST && APPLY)) {

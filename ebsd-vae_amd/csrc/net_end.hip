@@ -233,21 +233,24 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
 
   // ---- band partials, fixed order: lanes of a channel group in-wave, then the 4 waves
   const int lane = tid & 63, wave = tid >> 6;
-  double* red = reinterpret_cast<double*>(ne_sm);            // [2][4][NE_NTH]
+  // (a tree of lane shuffles: a serial 32-step LDS walk here cost ~8 us per block)
+  double* red = reinterpret_cast<double*>(ne_sm);            // [4 waves][8 cg][8]
 #pragma unroll
-  for (int k = 0; k < 4; ++k) { red[(0 * 4 + k) * NE_NTH + tid] = s1d[k]; red[(1 * 4 + k) * NE_NTH + tid] = s2d[k]; }
+  for (int k = 0; k < 8; ++k) {
+    double v = k < 4 ? s1d[k] : s2d[k - 4];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lane < 8) red[(wave * 8 + lane) * 8 + k] = v;
+  }
   __syncthreads();
   const int slice = b * T + tile;
-  if (tid < 8) {   // channel group tid: sum over its 32 pixel lanes in order
-    double u[4] = {0.0, 0.0, 0.0, 0.0}, v[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int p = 0; p < 32; ++p)
+  if (tid < C) {   // channel c = tid: group tid / 4, element tid % 4
+    const int g = tid >> 2, k = tid & 3;
+    double u = 0.0, v = 0.0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        u[k] += red[(0 * 4 + k) * NE_NTH + p * 8 + tid];
-        v[k] += red[(1 * 4 + k) * NE_NTH + p * 8 + tid];
-      }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) part[(size_t)slice * C + tid * 4 + k] = make_double2(u[k], v[k]);
+    for (int wv = 0; wv < 4; ++wv) { u += red[(wv * 8 + g) * 8 + k]; v += red[(wv * 8 + g) * 8 + 4 + k]; }
+    part[(size_t)slice * C + tid] = make_double2(u, v);
   }
   __syncthreads();
   // weight-gradient partials [slice][tap][0][ci]: fold the 32 pixel lanes of each channel group
