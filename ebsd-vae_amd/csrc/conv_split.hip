@@ -353,7 +353,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
                              float* __restrict__ y, float2* __restrict__ spart, int H, int W, int b0,
                              int h0, int wpx0, int mfs, int slot, int co_base, int hk, int l32,
                              const float* __restrict__ yprev, const float2* __restrict__ stprev,
-                             double2* __restrict__ ipart, float* __restrict__ ypool) {
+                             double2* __restrict__ ipart, float* __restrict__ ypool, float sc) {
   static_assert(MF % 2 == 0, "fragments in 64-pixel pairs");
   constexpr int NG = MF / 2;
   const int T = (H * W) / 64;
@@ -371,7 +371,9 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
     for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float v = acc[mf][nf][r] + bb;
+        // sc: the exact power-of-two undo of the f16 weight [and gradient] scale, so the fma
+        // rounds once, as (acc * sc) + bb did
+        const float v = fmaf(acc[mf][nf][r], sc, bb);
         acc[mf][nf][r] = v;
         s[mf >> 1] += v;
         if (FP != FP_UPSUM)
@@ -652,13 +654,21 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     return gs_k;
   };
 
+  // nch, H and TH are powers of two (plan_split), so the iteration -> (image, row, chunk) map
+  // is shifts and masks: no runtime integer division (a ~30-instruction SALU chain each) in
+  // the per-iteration instruction stream
+  const int lgnch = 31 - __builtin_clz(nch), lgH = 31 - __builtin_clz(H);
   auto coords = [&](int it, int& b0, int& h0, int& ch) EV_LAMBDA_INLINE {
-    const int tl = it / nch;
-    ch = it - tl * nch;
-    const int t = t0 + tl;
-    const int grp = t / tpi;
-    b0 = grp * NI;
-    h0 = (t - grp * tpi) * TH;
+    const int t = t0 + (it >> lgnch);
+    ch = it & (nch - 1);
+    if constexpr (NI == 1) {   // tile t = rows t*TH .. of the stacked images
+      const int r = t * TH;
+      b0 = r >> lgH;
+      h0 = r & (H - 1);
+    } else {                   // TH == H: tile t = images t*NI ..
+      b0 = t * NI;
+      h0 = 0;
+    }
   };
   // halo loads of iteration it into register slot sl: buffer loads with 32-bit offsets into
   // the tile's source image; rows above / below the image fall outside the descriptor's range
@@ -766,7 +776,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   // NP_F16: the layer's weight shift k (weights packed as w * 2^k), in the pack's trailer
   const int wshift = NP == NP_F16 ? *reinterpret_cast<const int*>(wp + (size_t)nch * WSLAB) : 0;
   auto issue_weights = [&](int it, char* lw) EV_LAMBDA_INLINE {
-    const int ch = it - (it / nch) * nch;
+    const int ch = it & (nch - 1);
 #pragma unroll
     for (int j = 0; j < WPER; ++j) {
       const int pc = wave_u + j * NWV;
@@ -790,20 +800,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     coords(it_done, b0, h0, ch);
     const int im = NI == 1 ? 0 : (wm * MW) / tpx;   // the wave's pixels lie in one image
     const int wpx0 = fpx0 - im * tpx;
+    float sc = 1.f;
     if constexpr (NP == NP_F16) {   // undo the weight [and gradient] scale (powers of two)
-      float sc = ldexpf(1.f, -wshift);
+      sc = ldexpf(1.f, -wshift);
       if constexpr (GS) sc = ldexpf(sc, -gshift(min(b0 + im, B - 1)));
-#pragma unroll
-      for (int mf = 0; mf < MF; ++mf)
-#pragma unroll
-        for (int nf = 0; nf < NF; ++nf)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[mf][nf][r] *= sc;
     }
     if (NI == 1 || b0 + im < B)
       pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
                                     (h0 * W + wm * MW - im * tpx) / 64, wn * NF * 32, hk, l32,
-                                    yprev, stprev, ipart, ypool);
+                                    yprev, stprev, ipart, ypool, sc);
   };
 
 #ifdef EV_PIPE_TRACE
@@ -1145,6 +1150,9 @@ struct X3Cfg {
 static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   if ((np != 2 && np != 3 && np != NP_F16) || cin % (2 * XCK) || !(cout == 128 || cout == 64 || cout == 32)) return false;
   if (np == NP_F16 && !use_pipe()) return false;
+  // the pipelined kernel maps iterations to (image, row band, chunk) by shifts
+  auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+  if (!pow2(cin / XCK) || !pow2(H) || !pow2(W)) return false;
   c->M = (np != 2 && cout != 128) ? 512 : 256;
   c->NI = 1;
   c->NT = cout;

@@ -115,6 +115,7 @@ static int wg_pipe_cot(int cout) {
 static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
   if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0) return false;
   if (H % 8 || W % 8 || cin % 32 || !(cout == 32 || cout % 64 == 0)) return false;
+  if (((H / 8) & (H / 8 - 1)) || ((W / 8) & (W / 8 - 1))) return false;   // tile_at shifts
   g->TW = 8; g->TH = 8; g->NI = 1;
   g->ntx = W / 8; g->nty = H / 8;
   g->lTW = 3; g->ltpx = 6;
@@ -816,9 +817,11 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
   float2 st_l[4], st_s[4];         // NORM: stats of the loading / the staging tile's image
   int lb = 0, ly = 0, lx = 0;      // tile whose data the item registers receive
   int sb = 0, sy = 0, sx = 0;      // tile being staged from them
+  // ntx and nty are powers of two (wg_pipe_geom): shifts, no runtime integer division
+  const int lgx = 31 - __builtin_clz(g.ntx), lgp = lgx + 31 - __builtin_clz(g.nty);
   auto tile_at = [&](int t, int& b0, int& y0, int& x0) EV_LAMBDA_INLINE {
-    const int ib = t / per_img, rr = t - ib * per_img, ty = rr / g.ntx;
-    b0 = ib; y0 = ty * T::TH; x0 = (rr - ty * g.ntx) * TW;
+    const int rr = t & ((1 << lgp) - 1);
+    b0 = t >> lgp; y0 = (rr >> lgx) * T::TH; x0 = (rr & (g.ntx - 1)) * TW;
   };
   // buffer loads with 32-bit offsets into the loading tile's image (scalar descriptor base,
   // tile-uniform offset + a per-lane constant): rows above / below the image and dead items
