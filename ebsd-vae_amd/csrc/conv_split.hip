@@ -348,14 +348,72 @@ EV_DEVINL void pipe_barrier() {
 //         of two (64 pixels) and every group writes one {mean, M2} (spart) or one fused-reduce
 //         double2 (ipart) slot, so every configuration has (H*W)/64 slots per image
 //   ypool FP_POOLOUT: the (H/2, W/2) max-pooled raw output (2x2 windows are lane-local)
-template <int MF, int NF, int FP, int NT>
+//   PH    0: the whole epilogue; with a fused IN-backward reduce of one 32-channel fragment
+//         column (pipe_prefetch_ok), PH 1 only loads the tile's y_prev values into pv (issued
+//         one iteration early, so their latency hides under that iteration's MFMAs) and PH 2
+//         is the epilogue reading them from pv instead of memory (same values, same order)
+template <int MF, int NF, int FP>
+constexpr bool pipe_prefetch_ok() { return NF == 1 && (FP == P_ID || FP == FP_UPSUM); }
+template <int MF, int NF, int FP>
+constexpr int pipe_prefetch_n() {
+  return pipe_prefetch_ok<MF, NF, FP>() ? (FP == FP_UPSUM ? 8 * (MF / 2) : 16 * MF) : 1;
+}
+template <int MF, int NF, int FP, int NT, int PH = 0>
 EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bias,
                              float* __restrict__ y, float2* __restrict__ spart, int H, int W, int b0,
                              int h0, int wpx0, int mfs, int slot, int co_base, int hk, int l32,
                              const float* __restrict__ yprev, const float2* __restrict__ stprev,
-                             double2* __restrict__ ipart, float* __restrict__ ypool, float sc) {
+                             double2* __restrict__ ipart, float* __restrict__ ypool, float sc,
+                             float (&pv)[pipe_prefetch_n<MF, NF, FP>()]) {
   static_assert(MF % 2 == 0, "fragments in 64-pixel pairs");
+  static_assert(PH == 0 || pipe_prefetch_ok<MF, NF, FP>(), "prefetch phases: NF 1, P_ID / UPSUM");
   constexpr int NG = MF / 2;
+  // input-gradient launches (a fused IN-backward reduce or the summed upsample adjoint) pass no
+  // statistics partials (spart == nullptr)
+  constexpr bool FUSED = FP == P_ID || FP == P_POOL || FP == P_UP || FP == FP_UPSUM;
+  if constexpr (PH == 1) {   // loads only: the offsets of the PH 0 / 2 code below
+    const int nf = 0;
+    const int co = co_base + l32;
+    if constexpr (FP == FP_UPSUM) {
+      const int W2 = W >> 1;
+      const auto rp = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(yprev + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int m0 = 2 * g;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          int prow, pc;
+          if (W >= 32) {
+            const int r = 2 * k;
+            prow = (wpx0 / W + m0) >> 1;
+            pc = ((wpx0 % W + 4 * hk) >> 1) + (((r & 3) + 8 * (r >> 2)) >> 1);
+          } else {
+            const int mf = m0 + (k >> 2), r = 2 * (k & 3);
+            prow = (wpx0 + mf * mfs) / W >> 1;
+            pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
+          }
+          pv[g * 8 + k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                        rp, ((prow * W2 + pc) * NT + co) * 4, 0, 0));
+        }
+      }
+    } else {
+      const int lW = 31 - __builtin_clz(W);
+      const int plane = H * W;
+      const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)(yprev + (size_t)b0 * plane * NT), 0,
+                                                        plane * NT * 4, 0x00020000);
+      const int pbase = h0 * W + wpx0 + 4 * hk;
+#pragma unroll
+      for (int e = 0; e < 16 * MF; ++e) {
+        const int mf = e >> 4, r = e & 15;
+        const int pl = pbase + mf * 32 + (r & 3) + 8 * (r >> 2);
+        pv[e] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rp, (inbwd_pix<FP>(pl, W, lW, 0) * NT + co) * 4, 0, 0));
+      }
+    }
+    (void)nf;
+    return;
+  }
   const int T = (H * W) / 64;
   const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ((size_t)b0 * H + h0) * W * NT), 0,
                                                     0x7fffffff, 0x00020000);
@@ -375,7 +433,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         // rounds once, as (acc * sc) + bb did
         const float v = fmaf(acc[mf][nf][r], sc, bb);
         acc[mf][nf][r] = v;
-        s[mf >> 1] += v;
+        if constexpr (!FUSED) s[mf >> 1] += v;   // input-gradient convs write no statistics
         if (FP != FP_UPSUM)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
                                                 vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
@@ -413,7 +471,8 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, 0));
+          v[k] = PH == 2 ? pv[g * 8 + k]
+                         : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, 0));
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, gs[k]), rq, off[k], 0, 0);
@@ -482,8 +541,9 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
             const int pl = pbase + mf * 32 + (r & 3) + 8 * (r >> 2);
 #pragma unroll
             for (int k = 0; k < NL; ++k)
-              v[j][k] = __builtin_bit_cast(
-                  float, __builtin_amdgcn_raw_buffer_load_b32(rp, (inbwd_pix<FP>(pl, W, lW, k) * NT + co) * 4, 0, 0));
+              v[j][k] = PH == 2 ? pv[e]
+                                : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                rp, (inbwd_pix<FP>(pl, W, lW, k) * NT + co) * 4, 0, 0));
           }
 #pragma unroll
           for (int j = 0; j < G; ++j) {
@@ -496,7 +556,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         if (hk == 0) ipart[((size_t)b0 * T + slot + g) * NT + co] = make_double2((double)s1, (double)s2);
       }
     }
-    if (spart) {
+    if (!FUSED && spart) {
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
         float sg = s[g];
@@ -532,7 +592,10 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 //     next iteration (after the barrier), so its stores drain under the next tile's MFMAs.
 // The old kernel paid each of these serially: one exposed global-load latency and one VALU
 // staging phase per chunk, plus the prologue / epilogue per tile (tools/conv_micro.py).
-template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI>
+//   WR > 0: the layer's WR = Cin / 8 weight slabs are loaded into LDS once, in the prologue,
+//   and stay resident (Cin = 32 layers, where they fit beside the halo buffers): no weight
+//   DMA per iteration (its issue cost sits in every iteration's instruction stream)
+template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI, int WR>
 __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, const char* __restrict__ wp,
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
@@ -554,6 +617,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr bool GS = (NP == NP_F16 && MODE == ACT_RAW);   // per-image gradient scale
   constexpr int PD = POOL ? 1 : 2;               // halo prefetch distance (iterations)
   static_assert(PD == 1 || KX * NR <= 7, "pipe_barrier keeps at most 7 loads in flight");
+  static_assert(WR == 0 || (PD == 2 && NI == 1), "resident weights: single-image, prefetch 2");
   extern __shared__ __attribute__((aligned(16))) char xsm[];
   // a tile is TH rows of one image, or NI whole images (NI > 1: TH == H); NI is a template
   // parameter so the single-image kernels carry none of the per-image bookkeeping
@@ -562,7 +626,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   const int pixP = NI * pixI;
   const int xslab = (pixP + 1) * XPS;
   char* lw0 = xsm;
-  char* lx0 = xsm + 2 * WSLABP;
+  char* lx0 = xsm + (WR ? WR * WSLAB : 2 * WSLABP);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -776,6 +840,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   // NP_F16: the layer's weight shift k (weights packed as w * 2^k), in the pack's trailer
   const int wshift = NP == NP_F16 ? *reinterpret_cast<const int*>(wp + (size_t)nch * WSLAB) : 0;
   auto issue_weights = [&](int it, char* lw) EV_LAMBDA_INLINE {
+    if constexpr (WR) return;   // resident since the prologue
     const int ch = it & (nch - 1);
 #pragma unroll
     for (int j = 0; j < WPER; ++j) {
@@ -795,6 +860,20 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
         for (int r = 0; r < 16; ++r) acc[mf][nf][r] = 0.f;
   };
   const int ncol = wn * NF * 32 + l32;
+  // fused IN-backward reduce of one fragment column: the tile's y_prev values are loaded at the
+  // start of its last iteration (pipe_epilogue PH 1) and consumed by its epilogue (PH 2)
+#ifdef EV_PIPE_NOPREF   // A/B: load them inside the epilogue
+  constexpr bool PREF = false;
+#else
+  constexpr bool PREF = pipe_prefetch_ok<MF, NF, FP>() && NI == 1;
+#endif
+  float pv[pipe_prefetch_n<MF, NF, FP>()];
+  auto epi_prefetch = [&](int it) EV_LAMBDA_INLINE {
+    int b0, h0, ch;
+    coords(it, b0, h0, ch);
+    pipe_epilogue<MF, NF, FP, NT, PREF ? 1 : 0>(acc, bias, y, spart, H, W, b0, h0, fpx0, mfs, 0,
+                                                wn * NF * 32, hk, l32, yprev, stprev, ipart, ypool, 1.f, pv);
+  };
   auto epilogue = [&](int it_done) EV_LAMBDA_INLINE {
     int b0, h0, ch;
     coords(it_done, b0, h0, ch);
@@ -805,10 +884,14 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
       sc = ldexpf(1.f, -wshift);
       if constexpr (GS) sc = ldexpf(sc, -gshift(min(b0 + im, B - 1)));
     }
+#ifdef EV_PIPE_NOEPI   // timing experiment only: no epilogue (no output, wrong results)
+    if (sc == 12345.f)
+#else
     if (NI == 1 || b0 + im < B)
-      pipe_epilogue<MF, NF, FP, NT>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
-                                    (h0 * W + wm * MW - im * tpx) / 64, wn * NF * 32, hk, l32,
-                                    yprev, stprev, ipart, ypool, sc);
+#endif
+      pipe_epilogue<MF, NF, FP, NT, PREF ? 2 : 0>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
+                                                  (h0 * W + wm * MW - im * tpx) / 64, wn * NF * 32, hk,
+                                                  l32, yprev, stprev, ipart, ypool, sc, pv);
   };
 
 #ifdef EV_PIPE_TRACE
@@ -825,6 +908,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     // unconditional issue (indices clamped at the end: the surplus loads land in buffers
     // nobody reads), so every iteration has the same vector-memory op count
     const int it1 = min(it + 1, nit - 1), itp = min(it + PD, nit - 1);
+    // the tile's last iteration (nch is even, so it is always a P = 1 one): its epilogue's
+    // y_prev loads go first, older than this iteration's halo loads, so the barrier's
+    // vmcnt(KX) retires them
+    if constexpr (PREF && P == 1)
+      if ((it & (nch - 1)) == nch - 1) epi_prefetch(it);
 #ifndef EV_PIPE_LATE_ISSUE
     issue_weights(it1, lw0 + (1 - P) * WSLABP);
     issue_halo(itp, std::integral_constant<int, SL_LD>());
@@ -834,7 +922,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     float2 fs[4];
     stage_fs(std::integral_constant<int, SL_ST>(), fs);
     const char* lx = lx0 + P * xslab;
-    const char* lw = lw0 + P * WSLABP;
+    const char* lw = WR ? lw0 + (it & (nch - 1)) * WSLAB : lw0 + P * WSLABP;
     char* lxn = lx0 + (1 - P) * xslab;
     // NF == 1: fragments of k-step s live in register set s & 1, the LDS reads of k-step s+1
     // are issued before the MFMAs of k-step s, so only k-step 0 waits on an LDS latency.
@@ -868,7 +956,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
       }
       bf16x8 (&a)[NPC][MF] = fa[fs_];
       bf16x8 (&b)[NPC][NF] = fb[fs_];
-#ifndef EV_PIPE_NOMFMA   // timing experiment only: one MFMA per fragment pair (wrong results)
+#if defined(EV_PIPE_NOMFMA2)   // timing experiment only: no MFMA at all, the fragments kept live
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf)
+          acc[mf][nf][0] += (float)a[0][mf][0] * (float)b[0][nf][0] + (float)a[1][mf][1] * (float)b[1][nf][1];
+#elif !defined(EV_PIPE_NOMFMA)   // timing experiment only: one MFMA per fragment pair (wrong results)
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
@@ -933,12 +1027,18 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     stage_post(std::integral_constant<int, SL_ST>(), fs, lxn);
     EV_TACC(tr_k, tb1);
     EV_T(tb2);
+#ifdef EV_PIPE_NOBAR   // timing experiment only: no barrier (LDS races, wrong results)
+    if (false) {
+#else
     if (PD == 2) {
+#endif
       // the halo loads of it+2 (this wave's youngest vector-memory ops) stay in flight across
       // the barrier: everything older -- the weight DMA of it+1, epilogue traffic -- is retired
       pipe_barrier<(PD == 2 ? KX * NR : 0)>();
     } else {
+#ifndef EV_PIPE_NOBAR
       __syncthreads();
+#endif
     }
     EV_TACC(tr_bar, tb2);
   };
@@ -962,7 +1062,14 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   }
   // prologue: weights + halo of it 0 (and the halo of it 1 for PD = 2)
   zero_acc();
-  issue_weights(0, lw0);
+  if constexpr (WR) {
+    // every chunk's slab, 1-KiB pieces over the waves (WR * WSLAB is whole pieces)
+    for (int pc = wave_u; pc < WR * WSLAB / 1024; pc += NWV)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwp, (lds_void_ptr)(lw0 + pc * 1024), 16,
+                                               pc * 1024 + lane * 16, 0, 0, 0);
+  } else {
+    issue_weights(0, lw0);
+  }
   issue_halo(0, std::integral_constant<int, 0>());
   {
     float2 fs[4];
@@ -972,6 +1079,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     for (int k = 0; k < KX; ++k)
       if (item_live(k)) stage_item(std::integral_constant<int, 0>(), k, fs, lx0);
     stage_post(std::integral_constant<int, 0>(), fs, lx0);
+  }
+  if constexpr (WR) {
+    // the resident slabs are older than both halo loads: all but the youngest (it 1's) landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KX * NR) : "memory");
   }
   __syncthreads();
   // nch = Cin / 8 is even for every supported layer (plan_split), so it & 1 == ch & 1
@@ -1122,6 +1233,15 @@ static bool use_multi_image() {
   return v != 0;
 }
 
+// EBSDVAE_WRES=0: Cin = 32 split-fp16 layers stream their weight slab per chunk (A/B timing)
+static bool use_wres() {
+  static const bool v = [] {
+    const char* e = getenv("EBSDVAE_WRES");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // compute units of the current device (cached per device id)
 static int cu_count() {
   static int cache[64] = {0};
@@ -1139,6 +1259,7 @@ static int cu_count() {
 struct X3Cfg {
   int M, TH, NT, KX, nwv;
   int NI;            // images per tile (> 1 only for the pipelined kernel on small maps)
+  int wr;            // pipelined split-fp16 kernel: resident weight slabs (Cin / 8), 0 = streamed
   size_t lds;        // conv3x3_split_kernel
   size_t lds_pipe;   // conv3x3_pipe_kernel (padded weight buffers); 0 = does not fit
 };
@@ -1191,6 +1312,14 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   c->lds = 2 * (size_t)wslab + 2 * (size_t)(pix + 1) * XPS;
   c->lds_pipe = 2 * (size_t)pipe_dma_per(wslab, c->nwv) * c->nwv * 1024 + 2 * (size_t)(pix + 1) * XPS;
   if (c->lds_pipe > 160 * 1024) c->lds_pipe = 0;
+  // Cin = 32 split-fp16 layers (4 chunks): all four weight slabs stay resident in LDS when they
+  // fit beside the two halo buffers (EBSDVAE_WRES=0 streams them per chunk, A/B)
+  c->wr = 0;
+  const size_t lds_wr = 4 * (size_t)wslab + 2 * (size_t)(pix + 1) * XPS;
+  if (np == NP_F16 && cin == 4 * XCK && c->NI == 1 && use_wres() && use_pipe() && lds_wr <= 160 * 1024) {
+    c->wr = 4;
+    c->lds_pipe = lds_wr;
+  }
   if (c->NI > 1 || np == NP_F16) return c->lds_pipe != 0;   // pipelined kernel only
   return c->lds <= 160 * 1024;
 }
@@ -1213,13 +1342,13 @@ static bool pipe_owns_images(const X3Cfg& c, int B, int H) {
   return tpb % tpi == 0;
 }
 
-template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI>
+template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI, int WR = 0>
 static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const void* wp,
                         const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                         int cin, hipStream_t s, const InBwdFuse& f) {
   const int ntiles = ((B + NI - 1) / NI) * (H / c.TH);
   if (NI > 1 || (use_pipe() && c.lds_pipe)) {
-    auto k = conv3x3_pipe_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP, NI>;
+    auto k = conv3x3_pipe_kernel<NP, NWV, WM, MF, NF, KX, MODE, FP, NI, WR>;
     static bool once = false;
     if (!once) {
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1247,34 +1376,34 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
   }
 }
 
-template <int NP, int NWV, int WM, int MF, int NF, int KX, int NI = 1>
+template <int NP, int NWV, int WM, int MF, int NF, int KX, int NI = 1, int WR = 0>
 static void launch_x3(const X3Cfg& c, const float* src, const float* st, int mode, const void* wp,
                       const float* bias, float* y, float* part, float* aout, int B, int H, int W,
                       int cin, hipStream_t s, int pmode, const InBwdFuse& f) {
   if (pmode >= 0) {
     switch (pmode) {
-      case P_ID: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_ID, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
-      case P_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_POOL, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+      case P_ID: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_ID, NI, WR>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+      case P_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_POOL, NI, WR>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
       case P_UPSUM:
         if constexpr (NI == 1)
-          launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_UPSUM, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f);
+          launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_UPSUM, NI, WR>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f);
         break;
-      default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_UP, NI>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
+      default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, P_UP, NI, WR>(c, src, nullptr, wp, nullptr, y, nullptr, nullptr, B, H, W, cin, s, f); break;
     }
     return;
   }
   if constexpr (NI == 1) {
     if (f.ypool) {   // producer of a max-pooled layer (ebsdvae_conv3x3_fwd_split_pooled)
-      launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM, FP_POOLOUT, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f);
+      launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM, FP_POOLOUT, NI, WR>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f);
       return;
     }
   }
   switch (mode) {
-    case ACT_RAW: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    case ACT_NORM: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    case ACT_NORM_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_POOL, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    case ACT_UP: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_UP, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
-    default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_UP, FP_NONE, NI>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_RAW: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_RAW, FP_NONE, NI, WR>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_NORM: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM, FP_NONE, NI, WR>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_NORM_POOL: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_POOL, FP_NONE, NI, 0>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    case ACT_UP: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_UP, FP_NONE, NI, WR>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
+    default: launch_x3_1<NP, NWV, WM, MF, NF, KX, ACT_NORM_UP, FP_NONE, NI, WR>(c, src, st, wp, bias, y, part, aout, B, H, W, cin, s, f); break;
   }
 }
 
@@ -1296,11 +1425,17 @@ static void dispatch_split(const X3Cfg& c, int np, const float* src, const float
       launch_x3<NP_F16, 4, 1, 2, 1, 1>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 128)
       launch_x3<NP_F16, 8, 4, 2, 2, 2>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else if (cout == 64 && c.wr)   // Cin = 32: weight slabs resident
+      launch_x3<NP_F16, 8, 8, 2, 2, 3, 1, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (cout == 64)
       launch_x3<NP_F16, 8, 8, 2, 2, 3>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else if (c.KX <= 3 && c.wr)
+      launch_x3<NP_F16, 8, 8, 2, 1, 3, 1, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
     else if (c.KX <= 3)
       launch_x3<NP_F16, 8, 8, 2, 1, 3>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
-    else   // 256-wide maps: two-row tiles, four items per thread
+    else if (c.wr)   // 256-wide maps: two-row tiles, four items per thread
+      launch_x3<NP_F16, 8, 8, 2, 1, 4, 1, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
+    else
       launch_x3<NP_F16, 8, 8, 2, 1, 4>(c, src, st, mode, wp, bias, y, part, aout, B, H, W, cin, s, pmode, f);
   } else {
     if (cout == 128 && c.NI > 1)   // two 8x8 images per tile: 2 x 4 waves of 64 px x 32 co
