@@ -330,6 +330,15 @@ constexpr int pipe_items_at(int s, int kx, int pd) {
   return n;
 }
 
+// Workgroup barrier with no vector-memory wait (resident-weight kernels: no LDS-DMA in the loop,
+// and every register load is waited for by the compiler where it is used): lgkmcnt(0) only
+EV_DEVINL void pipe_barrier_lds() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (3 << 14));   // vmcnt(63) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int N>
 EV_DEVINL void pipe_barrier() {
   static_assert(N >= 0 && N < 16, "vmcnt range");
@@ -874,7 +883,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     pipe_epilogue<MF, NF, FP, NT, PREF ? 1 : 0>(acc, bias, y, spart, H, W, b0, h0, fpx0, mfs, 0,
                                                 wn * NF * 32, hk, l32, yprev, stprev, ipart, ypool, 1.f, pv);
   };
-  auto epilogue = [&](int it_done) EV_LAMBDA_INLINE {
+  auto epilogue = [&](int it_done, f32x16 (&ea)[MF][NF]) EV_LAMBDA_INLINE {
     int b0, h0, ch;
     coords(it_done, b0, h0, ch);
     const int im = NI == 1 ? 0 : (wm * MW) / tpx;   // the wave's pixels lie in one image
@@ -889,7 +898,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #else
     if (NI == 1 || b0 + im < B)
 #endif
-      pipe_epilogue<MF, NF, FP, NT, PREF ? 2 : 0>(acc, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
+      pipe_epilogue<MF, NF, FP, NT, PREF ? 2 : 0>(ea, bias, y, spart, H, W, b0 + im, h0, wpx0, mfs,
                                                   (h0 * W + wm * MW - im * tpx) / 64, wn * NF * 32, hk,
                                                   l32, yprev, stprev, ipart, ypool, sc, pv);
   };
@@ -1034,7 +1043,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #endif
       // the halo loads of it+2 (this wave's youngest vector-memory ops) stay in flight across
       // the barrier: everything older -- the weight DMA of it+1, epilogue traffic -- is retired
-      pipe_barrier<(PD == 2 ? KX * NR : 0)>();
+      // (resident weights: no DMA to wait for)
+      if constexpr (WR > 0)
+        pipe_barrier_lds();
+      else
+        pipe_barrier<(PD == 2 ? KX * NR : 0)>();
     } else {
 #ifndef EV_PIPE_NOBAR
       __syncthreads();
@@ -1093,7 +1106,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     }
     // after the tile's last barrier: the stores drain under the next tile's MFMAs
     EV_T(te0);
-    epilogue(tl * nch);
+    epilogue(tl * nch, acc);
     zero_acc();
     EV_TACC(tr_epi, te0);
   }

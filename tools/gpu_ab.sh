@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=$R/gpurun_out
 cd $R
 NEW=$R/ebsd-vae_amd/lib/libebsdvae.so; OLD=$R/ebsd-vae_amd/lib/libebsdvae_old.so
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_trainer.py -x -q --timeout 300 --timeout-method thread > $O/t_$T.txt 2>&1 || { tail -30 $O/t_$T.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_trainer.py tests/test_gpu_fullsize.py -x -q --timeout 300 --timeout-method thread > $O/t_$T.txt 2>&1 || { tail -30 $O/t_$T.txt; exit 1; }
 tail -1 $O/t_$T.txt
 : > $O/micro_$T.txt
 for L in new old; do
