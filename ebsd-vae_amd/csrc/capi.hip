@@ -42,12 +42,17 @@ extern "C" int ebsdvae_version(void) { return 1; }
 // The ring is the signaler stream's device's (not the caller's current device), created
 // on that device; ring creation and the round-robin index are guarded, since forward and
 // autograd-backward threads both fork and join.
-extern "C" int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler) {
-  constexpr int kRing = 64, kMaxDev = 64;
-  static hipEvent_t ring[kMaxDev][kRing];
-  static int next[kMaxDev];
-  static bool made[kMaxDev];
-  static std::mutex mu;
+namespace {
+// ring[kind][device]: kind 0 = fork / join events (device-scope release, no timing), kind 1 =
+// kernel-attached fork events (signalled by the completion of the launch they are attached to)
+constexpr int kRing = 64, kMaxDev = 64;
+hipEvent_t g_ring[2][kMaxDev][kRing];
+int g_next[2][kMaxDev];
+bool g_made[2][kMaxDev];
+std::mutex g_mu;
+
+// the next event of the signaler stream's device's ring `kind` (created on first use)
+int ring_event(ebsdvae_stream_t signaler, int kind, hipEvent_t* out) {
   int dev = -1;
   if (signaler == nullptr || hipStreamGetDevice((hipStream_t)signaler, &dev) != hipSuccess) {
     if (hipGetDevice(&dev) != hipSuccess) dev = -1;
@@ -56,32 +61,76 @@ extern "C" int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t sig
     evh::set_error("stream_wait: no device for the signaler stream");
     return 2;
   }
-  hipEvent_t ev;
-  {
-    std::lock_guard<std::mutex> lock(mu);
-    if (!made[dev]) {
-      int cur = 0;
-      if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(dev) != hipSuccess) {
-        evh::set_error("stream_wait: cannot select device %d", dev);
-        return 2;
-      }
-      bool ok = true;
-      for (int i = 0; i < kRing && ok; ++i)
-        ok = hipEventCreateWithFlags(&ring[dev][i],
-                                     hipEventDisableTiming | hipEventReleaseToDevice) == hipSuccess;
-      (void)hipSetDevice(cur);
-      if (!ok) {
-        evh::set_error("stream_wait: hipEventCreateWithFlags failed");
-        return 2;
-      }
-      made[dev] = true;
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (!g_made[kind][dev]) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(dev) != hipSuccess) {
+      evh::set_error("stream_wait: cannot select device %d", dev);
+      return 2;
     }
-    ev = ring[dev][next[dev]];
-    next[dev] = (next[dev] + 1) % kRing;
+    bool ok = true;
+    for (int i = 0; i < kRing && ok; ++i)
+      ok = hipEventCreateWithFlags(&g_ring[kind][dev][i],
+                                   kind == 0 ? (hipEventDisableTiming | hipEventReleaseToDevice)
+                                             : hipEventDefault) == hipSuccess;
+    (void)hipSetDevice(cur);
+    if (!ok) {
+      evh::set_error("stream_wait: hipEventCreateWithFlags failed");
+      return 2;
+    }
+    g_made[kind][dev] = true;
   }
+  *out = g_ring[kind][dev][g_next[kind][dev]];
+  g_next[kind][dev] = (g_next[kind][dev] + 1) % kRing;
+  return 0;
+}
+
+// kernel-attached fork (ebsdvae_fork_arm / ebsdvae_fork_wait), per host thread: the forward and
+// the autograd backward threads each arm and consume their own
+thread_local hipEvent_t g_fork_ev = nullptr;
+thread_local int g_fork_state = 0;   // 0 none, 1 armed, 2 attached to a launch
+}  // namespace
+
+namespace evh {
+hipEvent_t take_fork_event() {
+  if (g_fork_state != 1) return nullptr;
+  g_fork_state = 2;
+  return g_fork_ev;
+}
+}  // namespace evh
+
+extern "C" int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler) {
+  hipEvent_t ev;
+  if (ring_event(signaler, 0, &ev)) return 2;
   if (hipEventRecord(ev, (hipStream_t)signaler) != hipSuccess ||
       hipStreamWaitEvent((hipStream_t)waiter, ev, 0) != hipSuccess) {
     evh::set_error("stream_wait: %s", hipGetErrorString(hipGetLastError()));
+    return 2;
+  }
+  return 0;
+}
+
+// Fork without an event record on the signaler: the next launch of the InstanceNorm-backward
+// apply (the kernel that produces the weight gradient's gy) carries an event that its own
+// completion signals (hipExtLaunchKernel stopEvent), and ebsdvae_fork_wait makes the waiter
+// wait on it.  A record packet on the main stream between the apply and the input-gradient
+// conv left the GPU idle for ~7 us per fork (tools/step_gaps.py).
+extern "C" int ebsdvae_fork_arm(ebsdvae_stream_t signaler) {
+  hipEvent_t ev;
+  if (ring_event(signaler, 1, &ev)) return 2;
+  g_fork_ev = ev;
+  g_fork_state = 1;
+  return 0;
+}
+
+// `waiter` waits for the armed launch if one took the event; otherwise (nothing launched since
+// the arm) it falls back to ebsdvae_stream_wait on `signaler`.  Disarms either way.
+extern "C" int ebsdvae_fork_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler) {
+  const int st = g_fork_state;
+  g_fork_state = 0;
+  if (st != 2) return ebsdvae_stream_wait(waiter, signaler);
+  if (hipStreamWaitEvent((hipStream_t)waiter, g_fork_ev, 0) != hipSuccess) {
+    evh::set_error("fork_wait: %s", hipGetErrorString(hipGetLastError()));
     return 2;
   }
   return 0;

@@ -179,6 +179,9 @@ EV_DEVINL int f16_gshift(const float* __restrict__ gmax, int gmT, int b) {
 namespace evh {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// the event armed by ebsdvae_fork_arm for the next gy-producing launch (nullptr if none); the
+// caller attaches it to that launch (hipExtLaunchKernel stopEvent)
+hipEvent_t take_fork_event();
 }  // namespace evh
 
 // a spatial extent the shape queries accept (H * W and its multiples stay inside int)

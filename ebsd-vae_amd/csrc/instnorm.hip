@@ -11,6 +11,8 @@
 //   g_y    = rstd * (g_xhat - mean(g_xhat) - xhat * mean(g_xhat * xhat))
 // two HBM-bound passes (reduce, apply) over NHWC planes with float4 channel vectors; the
 // plane sums use fixed-order two-level reductions (deterministic).
+#include <hip/hip_ext.h>
+
 #include "common.h"
 #include "instnorm_fin.h"
 #include "../../include/ebsdvae.h"
@@ -585,9 +587,16 @@ extern "C" int ebsdvae_in_bwd_apply_max(const float* gnext, int pmode, const flo
   EV_REQUIRE(gnext && y && stats && bstats && gy, "in_bwd_apply: null pointer");
   EV_REQUIRE(pmode >= 0 && pmode <= 2 && C % 4 == 0 && (256 % (C / 4)) == 0, "in_bwd_apply: bad pmode/C");
   const int T = in_bwd_apply_tiles_host(B, H, W);
-  hipLaunchKernelGGL(in_bwd_kernel<true>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
-                     pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy, H,
-                     W, C, T, gmax);
+  // an armed side-stream fork (ebsdvae_fork_arm) rides on this launch's completion signal
+  if (hipEvent_t fe = evh::take_fork_event()) {
+    hipExtLaunchKernelGGL(in_bwd_kernel<true>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, nullptr,
+                          fe, 0, gnext, pmode, y, (const float2*)stats, (const float2*)bstats,
+                          (double2*)nullptr, gy, H, W, C, T, gmax);
+  } else {
+    hipLaunchKernelGGL(in_bwd_kernel<true>, dim3(T, B), dim3(256), 0, (hipStream_t)stream, gnext,
+                       pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy,
+                       H, W, C, T, gmax);
+  }
   return evh::check_launch("in_bwd_apply");
 }
 

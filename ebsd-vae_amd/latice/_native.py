@@ -26,6 +26,8 @@ SIGNATURES = {
     "ebsdvae_last_error": [],
     "ebsdvae_version": [],
     "ebsdvae_stream_wait": [P, P],
+    "ebsdvae_fork_arm": [P],
+    "ebsdvae_fork_wait": [P, P],
     "ebsdvae_conv_first_stat_tiles": [I, I],
     "ebsdvae_conv_first_fwd": [P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_apply_wgrad_rc": [P, P, P, P, P, P, P, P, I, I, I, I, P],

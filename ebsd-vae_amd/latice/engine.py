@@ -21,6 +21,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
+import threading
 import weakref
 from dataclasses import dataclass, field
 
@@ -602,11 +603,33 @@ def stream_wait(waiter, signaler):
         waiter.wait_stream(signaler)
 
 
+# EBSDVAE_KFORK=0: every fork records an event on the main stream (A/B).  Otherwise the
+# backward arms a kernel-attached fork before each InstanceNorm-backward apply whose gy a
+# weight gradient takes: the apply launch itself signals the event (ebsdvae_fork_arm /
+# ebsdvae_fork_wait), so no record packet sits between the apply and the input-gradient conv.
+_KFORK = os.environ.get("EBSDVAE_KFORK", "1") != "0"
+_FORK = threading.local()
+
+
+def fork_arm(device):
+    """Arm a kernel-attached fork for the next InstanceNorm-backward apply on the current
+    stream (no-op when the weight gradients will not go to the side stream)."""
+    if _KFORK and _LIGHT_EVENTS and _side_stream(device) is not None \
+            and not torch.cuda.is_current_stream_capturing():
+        N.call("ebsdvae_fork_arm", N.stream())
+        _FORK.armed = True
+
+
 def _side_use(device, *tensors):
     """Fork the side stream from the current stream and keep `tensors` alive until the join."""
     key = _dev_key(device)
     side = side_stream(device)
-    stream_wait(side, torch.cuda.current_stream(device))
+    cur = torch.cuda.current_stream(device)
+    if getattr(_FORK, "armed", False):
+        _FORK.armed = False
+        N.call("ebsdvae_fork_wait", side.cuda_stream, cur.cuda_stream)
+    else:
+        stream_wait(side, cur)
     keep = _KEEP.get(key)
     if keep is None:
         keep = _KEEP[key] = []
@@ -1031,6 +1054,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
             in_backward_first(g_next, y, st, x, dw, db, part=part, w0=params[wn], b0=params[bn])
             out[wn], out[bn] = dw, db
             break
+        fork_arm(y.device)   # the weight gradient below forks on the apply's completion
         gy = in_backward(g_next, L.pmode, y, st, part=part)
         mode = L.src_mode
         if i == 0:
@@ -1172,6 +1196,7 @@ def _decoder_backward(plan, g_xhat, saved, params, grads, packs, end=None):
             gy = gy_last
         else:   # a summed upsample adjoint (conv_dgrad sum_up) arrives at y's resolution
             pm = P_ID if (L.pmode == P_UP and g_next.shape[1] == y.shape[1]) else L.pmode
+            fork_arm(y.device)   # the weight gradient below forks on the apply's completion
             gy = in_backward(g_next, pm, y, st, part=part)
         wn, bn = L.name + ".weight", L.name + ".bias"
         src, sst = (saved["__dec_in__"], None) if i == 0 else saved[plan.dec[i - 1].name]

@@ -43,6 +43,12 @@ int ebsdvae_version(void);
  * release: cheaper than the default system-scope fence of torch's Stream.wait_stream).
  * Used for the weight-gradient side stream's fork / join (latice/engine.py); capturable. */
 int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler);
+/* Kernel-attached fork (no record packet on the signaler): arm, launch the InstanceNorm-backward
+ * apply (ebsdvae_in_bwd_apply[_max]) on `signaler`, then ebsdvae_fork_wait makes `waiter` wait
+ * for that launch's completion (falls back to ebsdvae_stream_wait when nothing took the event).
+ * Per host thread. */
+int ebsdvae_fork_arm(ebsdvae_stream_t signaler);
+int ebsdvae_fork_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler);
 
 /* ---- weights ------------------------------------------------------------------------
  * Pack a Conv2d (kind 0: (cout,cin,3,3), latice/model.py:95,148) or ConvTranspose2d
