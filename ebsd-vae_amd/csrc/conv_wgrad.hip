@@ -100,15 +100,17 @@ static bool wg_pipe() {
   }();
   return v;
 }
-// output channels per block of the pipelined kernel: 32 (cout 32), 64, or -- with
-// EBSDVAE_WG_CO128=1 -- 128 (8-wave blocks, one per CU, for cout % 128 == 0).  Alone the wide
-// blocks stage 1.28x fewer elements per FLOP and run 7-8 % faster (128->128 @32 232 -> 215 us,
-// 64->128 @32 116 -> 107 us), but the step got ~0.1 ms slower: a 112-KB block owns its CU, so
-// the weight gradients on the side stream crowd out the input-gradient chain beside them.
+// output channels per block of the pipelined kernel: 32 (cout 32), 128 (8-wave blocks, one per
+// CU, for cout % 128 == 0) or 64 (cout 64; every cout % 64 == 0 with EBSDVAE_WG_CO128=0).  Alone
+// the wide blocks stage 1.28x fewer elements per FLOP and run 7-8 % faster (128->128 @32 232 ->
+// 215 us, 64->128 @32 116 -> 107 us).  In round 2's step they were ~0.1 ms slower (a 112-KB
+// block owns its CU and crowded out the input-gradient chain beside it); with round 3's
+// schedule (kernel-attached forks, fused network end) the step is 0.07 ms faster with them
+// (two pairs, same box), so they are the default.
 static int wg_pipe_cot(int cout) {
   static const bool wide = [] {
     const char* e = getenv("EBSDVAE_WG_CO128");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return cout == 32 ? 32 : ((wide && cout % 128 == 0) ? 128 : 64);
 }
