@@ -21,7 +21,6 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
-import threading
 import weakref
 from dataclasses import dataclass, field
 
@@ -608,25 +607,29 @@ def stream_wait(waiter, signaler):
 # weight gradient takes: the apply launch itself signals the event (ebsdvae_fork_arm /
 # ebsdvae_fork_wait), so no record packet sits between the apply and the input-gradient conv.
 _KFORK = os.environ.get("EBSDVAE_KFORK", "1") != "0"
-_FORK = threading.local()
 
 
-def fork_arm(device):
+def fork_arm(device) -> bool:
     """Arm a kernel-attached fork for the next InstanceNorm-backward apply on the current
-    stream (no-op when the weight gradients will not go to the side stream)."""
+    stream.  Returns the token to pass to the weight gradient that consumes that apply's gy
+    (conv_wgrad(..., fork=...)); False (nothing armed) when the weight gradients will not go
+    to the side stream.  The armed state lives in the library per host thread: a later arm
+    replaces it, and only a conv_wgrad holding the token waits on it."""
     if _KFORK and _LIGHT_EVENTS and _side_stream(device) is not None \
             and not torch.cuda.is_current_stream_capturing():
         N.call("ebsdvae_fork_arm", N.stream())
-        _FORK.armed = True
+        return True
+    return False
 
 
-def _side_use(device, *tensors):
-    """Fork the side stream from the current stream and keep `tensors` alive until the join."""
+def _side_use(device, *tensors, fork=False):
+    """Fork the side stream from the current stream and keep `tensors` alive until the join.
+    fork: fork_arm()'s token -- the side stream waits for the armed apply launch only (the
+    last main-stream work the caller's inputs depend on) instead of an event recorded now."""
     key = _dev_key(device)
     side = side_stream(device)
     cur = torch.cuda.current_stream(device)
-    if getattr(_FORK, "armed", False):
-        _FORK.armed = False
+    if fork:
         N.call("ebsdvae_fork_wait", side.cuda_stream, cur.cuda_stream)
     else:
         stream_wait(side, cur)
@@ -835,7 +838,8 @@ def in_backward_first(gnext, y, st, x, dw0, db0, part=None, w0=None, b0=None):
     _reduce_slices(wpart, bpart, S_, 1, C, KIND_CONV, dw0, db0)
 
 
-def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized=None):
+def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized=None,
+               fork=False):
     """normalized: src is a normalised activation (default: the NORM modes); the split-fp16
     weight gradient (f16x3, gy with per-tile maxima) scales only gy, so it needs one.
     Runs on the side stream (see _side_stream); dw/db are written by the slice reduction on
@@ -843,7 +847,7 @@ def conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized
     side = _side_stream(gy.device)
     if side is None:
         return _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalized)
-    side = _side_use(gy.device, src, src_stats, gy, getattr(gy, "ev_gmax", None))
+    side = _side_use(gy.device, src, src_stats, gy, getattr(gy, "ev_gmax", None), fork=fork)
     with torch.cuda.stream(side):
         wpart, bpart, S_ = _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db,
                                        normalized, reduce=False)
@@ -1054,7 +1058,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
             in_backward_first(g_next, y, st, x, dw, db, part=part, w0=params[wn], b0=params[bn])
             out[wn], out[bn] = dw, db
             break
-        fork_arm(y.device)   # the weight gradient below forks on the apply's completion
+        fk = fork_arm(y.device)   # the weight gradient below forks on the apply's completion
         gy = in_backward(g_next, L.pmode, y, st, part=part)
         mode = L.src_mode
         if i == 0:
@@ -1069,7 +1073,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
         dw = _grad_buf(grads, wn, params[wn])
         db = _grad_buf(grads, bn, params[bn])
         # every source but the raw input image is a normalised activation (.act_in included)
-        conv_wgrad(src, sst, mode, gy, L.cin, L.cout, L.kind, dw, db, normalized=i > 0)
+        conv_wgrad(src, sst, mode, gy, L.cin, L.cout, L.kind, dw, db, normalized=i > 0, fork=fk)
         out[wn], out[bn] = dw, db
         if i > 0:
             P = plan.enc[i - 1]
@@ -1192,17 +1196,18 @@ def _decoder_backward(plan, g_xhat, saved, params, grads, packs, end=None):
     for i in reversed(range(len(plan.dec))):
         L = plan.dec[i]
         y, st = saved[L.name]
+        fk = False
         if i == len(plan.dec) - 1:
             gy = gy_last
         else:   # a summed upsample adjoint (conv_dgrad sum_up) arrives at y's resolution
             pm = P_ID if (L.pmode == P_UP and g_next.shape[1] == y.shape[1]) else L.pmode
-            fork_arm(y.device)   # the weight gradient below forks on the apply's completion
+            fk = fork_arm(y.device)   # the weight gradient below forks on the apply's completion
             gy = in_backward(g_next, pm, y, st, part=part)
         wn, bn = L.name + ".weight", L.name + ".bias"
         src, sst = (saved["__dec_in__"], None) if i == 0 else saved[plan.dec[i - 1].name]
         dw = _grad_buf(grads, wn, params[wn])
         db = _grad_buf(grads, bn, params[bn])
-        conv_wgrad(src, sst, L.src_mode, gy, L.cin, L.cout, L.kind, dw, db)
+        conv_wgrad(src, sst, L.src_mode, gy, L.cin, L.cout, L.kind, dw, db, fork=fk)
         out[wn], out[bn] = dw, db
         if i > 0:
             P = plan.dec[i - 1]
