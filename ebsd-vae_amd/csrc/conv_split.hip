@@ -443,7 +443,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         const float v = fmaf(acc[mf][nf][r], sc, bb);
         acc[mf][nf][r] = v;
         if constexpr (!FUSED) s[mf >> 1] += v;   // input-gradient convs write no statistics
-        if (FP != FP_UPSUM)
+        if (FP != FP_UPSUM && (FP != FP_POOLOUT || y))   // pooled inference: ypool only
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
                                                 vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
       }
@@ -1617,7 +1617,7 @@ extern "C" int ebsdvae_conv3x3_fwd_split_st(const float* src, const float* src_s
                                             int H, int W, int cin, int cout, int pieces,
                                             ebsdvae_stream_t stream) {
   X3Cfg c;
-  EV_REQUIRE(src && wpack && y && stat_part && st && B > 0,
+  EV_REQUIRE(src && wpack && (y || ypool) && stat_part && st && B > 0,
              "conv3x3_fwd_split_st: null pointer or empty batch");
   EV_REQUIRE(src_mode >= 0 && src_mode <= 4, "conv3x3_fwd_split_st: bad src_mode %d", src_mode);
   EV_REQUIRE(src_mode == ACT_RAW || src_mode == ACT_UP || src_stats,

@@ -413,6 +413,9 @@ def pool_out_ok(layer: ConvLayer, wp) -> bool:
 # the first block's backward can recompute y0 from x bit-identically instead of re-reading it
 # (ebsdvae_in_bwd_first_apply_wgrad_rc).  EBSDVAE_FIRST_VALU=0: the fp32-MFMA conv + re-read.
 _FIRST_VALU = os.environ.get("EBSDVAE_FIRST_VALU", "1") != "0"
+# inference skips the full-resolution output of pooled producers (ypool only);
+# EBSDVAE_EVAL_Y=1 writes it anyway, for A/B timing
+_EVAL_Y = os.environ.get("EBSDVAE_EVAL_Y", "0") == "1"
 
 
 def _first_valu(layer: ConvLayer) -> bool:
@@ -437,20 +440,21 @@ def _conv_first(x, layer: ConvLayer, w, b, B):
 
 
 def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=None, mode=None,
-                 pool_out=False):
+                 pool_out=False, keep_y=True):
     """One conv block forward: y (B,H,H,cout) pre-norm + IN stats {mean,rstd} (B,cout,2).
     keep_act: also return the conv's logical input (materialised by the kernel), used by
     max-pool-fed layers so their wgrad reads the pooled tensor.  wp: pre-packed weight.
     mode: source mode override (a max-pool-fed layer reading its producer's pooled output
     in ACT_NORM mode).  pool_out: also return ypool = 2x2 max of y (B,H/2,H/2,cout), the
-    producer side of that (ebsdvae_conv3x3_fwd_split_pooled)."""
+    producer side of that (ebsdvae_conv3x3_fwd_split_pooled); keep_y=False with pool_out
+    (inference) writes ypool only and returns y None."""
     H = layer.H
     src_mode = layer.src_mode if mode is None else mode
     if src_mode == ACT_RAW and not keep_act and not pool_out and _first_valu(layer):
         return _conv_first(src, layer, w, b, B)
     if wp is None:
         wp = pack_weight(w, layer, dgrad=False)
-    y = _empty(B, H, H, layer.cout, like=w)
+    y = _empty(B, H, H, layer.cout, like=w) if keep_y or not pool_out else None
     T = N.call("ebsdvae_conv3x3_split_stat_tiles" if wp.pieces else "ebsdvae_conv3x3_stat_tiles",
                H, H, layer.cout)
     part = _empty(B, T, layer.cout, 2, like=w)
@@ -459,7 +463,8 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
     args = (N.ptr(src), N.ptr(src_stats), src_mode, N.ptr(wp.t), N.ptr(b), N.ptr(y),
             N.ptr(part), N.ptr(act), B, H, H, layer.cin, layer.cout)
     flops = conv_flops(B, H, H, layer.cin, layer.cout)
-    nb = 4 * (src.numel() + y.numel() + (y.numel() // 4 if pool_out else 0))   # algorithmic I/O
+    ny = B * H * H * layer.cout
+    nb = 4 * (src.numel() + (ny if y is not None else 0) + (ny // 4 if pool_out else 0))   # algorithmic I/O
     ypool = None
     st = _empty(B, layer.cout, 2, like=w)
     if pool_out:
@@ -1020,8 +1025,9 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True, packs_ready=N
         elif train and L.src_mode == ACT_NORM_POOL:
             y, st, act = conv_forward(src, sst, L, w, b, B, keep_act=True, wp=wp)
             saved[L.name + ".act_in"] = act
-        elif pool_out:
-            y, st, ypool = conv_forward(src, sst, L, w, b, B, wp=wp, pool_out=True)
+        elif pool_out:   # inference: only the pooled output is read downstream
+            y, st, ypool = conv_forward(src, sst, L, w, b, B, wp=wp, pool_out=True,
+                                        keep_y=train or _EVAL_Y)
         else:
             y, st = conv_forward(src, sst, L, w, b, B, wp=wp)
         pooled = ypool if pool_out else None

@@ -181,7 +181,8 @@ int ebsdvae_conv3x3_dgrad_inbwd_f16(const float* g, const float* gmax, int gm_ti
  * standalone finalize; bit-identical either way, EBSDVAE_FUSE_FINALIZE=0 forces the latter):
  *   _fwd_split_st: ebsdvae_conv3x3_fwd_split (ypool = NULL) or _fwd_split_pooled (ypool set),
  *     then ebsdvae_in_stats_finalize(stat_part, st, B, cout, tiles, H*W/tiles) -> st (B, cout)
- *     {mean, rstd};
+ *     {mean, rstd}; with ypool set, y may be NULL (inference: the full-resolution output is
+ *     then not written, st and ypool are unchanged);
  *   _dgrad_inbwd_f16_bst: ebsdvae_conv3x3_dgrad_inbwd_f16 with pmode >= 0, then
  *     ebsdvae_in_bwd_finalize(part, bst, B, cout, tiles, prev_hw) -> bst (B, cout), with
  *     (cin, cout) the channels of g and gin as in ebsdvae_conv3x3_dgrad_inbwd_f16 and prev_hw
