@@ -27,10 +27,13 @@ constexpr int FP_POOLOUT = 3;
 constexpr int FP_UPSUM = 4;
 
 // Fused InstanceNorm-backward reduce of the PREVIOUS block (input-gradient convs only):
-// this conv's output is g = d loss / d a_prev (a_prev = [pool|up](lrelu(IN(y_prev))) at
-// this conv's resolution).  Per element it adds g_a = g * lrelu'(xhat) and g_a * xhat of
+// this conv's product is g = d loss / d a_prev (a_prev = [pool|up](lrelu(IN(y_prev))) at
+// this conv's resolution).  Per element it adds h = g * lrelu'(xhat) and h * xhat of
 // the y_prev pixel that g routes to (identity, the 2x2 argmax, or the upsample parent)
-// -- the sums ebsdvae_in_bwd_reduce would compute, without re-reading g.
+// -- the sums ebsdvae_in_bwd_reduce would compute, without re-reading g -- and the conv
+// writes h, not g: every consumer of a fused input gradient (the InstanceNorm-backward
+// apply, the first block's pass, the gy-staging input-gradient conv) needs h, and the
+// LeakyReLU branch is then taken once, where the reduce takes it.
 // y_prev offset (in pixels of y_prev) of the k-th value read for conv pixel pl
 template <int FP>
 EV_DEVINL int inbwd_pix(int pl, int W, int lW, int k) {
@@ -41,7 +44,7 @@ EV_DEVINL int inbwd_pix(int pl, int W, int lW, int k) {
 }
 
 template <int FP>
-EV_DEVINL void inbwd_acc(float g, const float* v, float2 sp, float& s1, float& s2) {
+EV_DEVINL float inbwd_acc(float g, const float* v, float2 sp, float& s1, float& s2) {
   float x = (v[0] - sp.x) * sp.y;
   if (FP == P_POOL) {   // first maximum of lrelu(xhat) in window order (0,0),(0,1),(1,0),(1,1)
     float best = lrelu(x);
@@ -55,6 +58,7 @@ EV_DEVINL void inbwd_acc(float g, const float* v, float2 sp, float& s1, float& s
   const float ga = g * slope(x);
   s1 += ga;
   s2 = fmaf(ga, x, s2);
+  return ga;
 }
 
 template <int MF, int NF, int FP, int GMAX = 32>
@@ -83,9 +87,8 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         const float v = acc[mf][nf][r] + bb;
         acc[mf][nf][r] = v;
         s += v;
-#ifndef EV_TIMING_PROBE_NOEPI   // timing experiment only: no output traffic (wrong results)
-        if (bvalid) y[(((size_t)gb * H + h0) * W + rem) * Cout + co] = v;
-#endif
+        // a fused input gradient writes h (below), the forward its pre-norm output
+        if (FP == FP_NONE && bvalid) y[(((size_t)gb * H + h0) * W + rem) * Cout + co] = v;
       }
     if (FP != FP_NONE && bvalid) {
       // loads in batches of GMAX values issued before any use (latency overlapped within a batch)
@@ -110,8 +113,10 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         }
 #pragma unroll
         for (int j = 0; j < G; ++j) {
-          const int e = e0 + j;
-          inbwd_acc<FP>(acc[e >> 4][nf][e & 15], v[j], sp, s1, s2);
+          const int e = e0 + j, mf = e >> 4, r = e & 15;
+          const float h = inbwd_acc<FP>(acc[mf][nf][r], v[j], sp, s1, s2);
+          const int rem = wpx0 + mf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk - wimg * tpx;
+          y[(((size_t)gb * H + h0) * W + rem) * Cout + co] = h;
         }
       }
       s1 += __shfl_xor(s1, 32, 64);

@@ -357,6 +357,7 @@ EV_DEVINL void pipe_barrier() {
 //         of two (64 pixels) and every group writes one {mean, M2} (spart) or one fused-reduce
 //         double2 (ipart) slot, so every configuration has (H*W)/64 slots per image
 //   ypool FP_POOLOUT: the (H/2, W/2) max-pooled raw output (2x2 windows are lane-local)
+//   Fused input-gradient launches write h = g * lrelu'(xhat), not g (conv_common.h).
 //   PH    0: the whole epilogue; with a fused IN-backward reduce of one 32-channel fragment
 //         column (pipe_prefetch_ok), PH 1 only loads the tile's y_prev values into pv (issued
 //         one iteration early, so their latency hides under that iteration's MFMAs) and PH 2
@@ -443,7 +444,8 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         const float v = fmaf(acc[mf][nf][r], sc, bb);
         acc[mf][nf][r] = v;
         if constexpr (!FUSED) s[mf >> 1] += v;   // input-gradient convs write no statistics
-        if (FP != FP_UPSUM && (FP != FP_POOLOUT || y))   // pooled inference: ypool only
+        // fused input gradients write h (below); pooled inference writes ypool only
+        if (!FUSED && (FP != FP_POOLOUT || y))
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
                                                 vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
       }
@@ -482,12 +484,12 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         for (int k = 0; k < 8; ++k)
           v[k] = PH == 2 ? pv[g * 8 + k]
                          : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, 0));
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, gs[k]), rq, off[k], 0, 0);
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) inbwd_acc<P_ID>(gs[k], &v[k], sp, s1, s2);
+        for (int k = 0; k < 8; ++k) {
+          const float h = inbwd_acc<P_ID>(gs[k], &v[k], sp, s1, s2);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), rq, off[k], 0, 0);
+        }
         s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 32, 64);
         if (hk == 0) ipart[((size_t)b0 * T + slot + g) * NT + co] = make_double2((double)s1, (double)s2);
@@ -556,8 +558,10 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
           }
 #pragma unroll
           for (int j = 0; j < G; ++j) {
-            const int e = e0 + j;
-            inbwd_acc<FP>(acc[e >> 4][nf][e & 15], v[j], sp, s1, s2);
+            const int e = e0 + j, mf = e >> 4, r = e & 15;
+            const float h = inbwd_acc<FP>(acc[mf][nf][r], v[j], sp, s1, s2);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), ry,
+                                                  vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
           }
         }
         s1 += __shfl_xor(s1, 32, 64);

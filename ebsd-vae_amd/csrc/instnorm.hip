@@ -69,7 +69,9 @@ static int in_bwd_tiles_host(int H, int W) {
   return T;
 }
 
-template <bool APPLY>
+// HIN (apply only): gnext is h = g * lrelu'(xhat) at the routed pixel -- the output of a fused
+// input-gradient conv (conv_common.h) -- so the LeakyReLU factor is already in it
+template <bool APPLY, bool HIN = false>
 __global__ __launch_bounds__(256) void in_bwd_kernel(
     const float* __restrict__ gnext, int pmode, const float* __restrict__ y,
     const float2* __restrict__ st, const float2* __restrict__ bst, double2* __restrict__ part,
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
 #pragma unroll
           for (int ch = 0; ch < 4; ++ch) {
             const float x = xh[k][ch];
-            const float gx = (arg[ch] == k) ? gv[ch] * slope(x) : 0.f;
+            const float gx = (arg[ch] == k) ? (HIN ? gv[ch] : gv[ch] * slope(x)) : 0.f;
             o[ch] = rstd[ch] * (gx - m1[ch] - x * m2[ch]);
             amax = fmaxf(amax, fabsf(o[ch]));
           }
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
 #pragma unroll
       for (int ch = 0; ch < 4; ++ch) {
         const float x = (yy[ch] - mean[ch]) * rstd[ch];
-        const float gx = gv[ch] * slope(x);
+        const float gx = HIN ? gv[ch] : gv[ch] * slope(x);
         if (!APPLY) {
           a1[ch] += (double)gx;
           a2[ch] = fma((double)gx, (double)x, a2[ch]);
@@ -247,7 +249,8 @@ EV_DEVINL void wave_fold8(float& v) {  // sum over the 8 pixel rows of a wave (l
   v += __shfl_xor(v, 32, 64);
 }
 
-template <int FUSE, bool APPLY>
+// HIN (FIRST apply only): gsrc is h (the fused input gradient's output), not g
+template <int FUSE, bool APPLY, bool HIN = false>
 __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     const float* __restrict__ gsrc, const float* __restrict__ w14, const float* __restrict__ y,
     const float2* __restrict__ st, const float2* __restrict__ bst, const float* __restrict__ x,
@@ -392,7 +395,7 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float xh = (yy[k] - mean[k]) * rstd[k];
-      const float gx = ga[k] * slope(xh);
+      const float gx = (HIN && FUSE_ == FUSE_FIRST) ? ga[k] : ga[k] * slope(xh);
       if (!APPLY) {
         a1[k] += (double)gx;
         a2[k] = fma((double)gx, (double)xh, a2[k]);
@@ -600,6 +603,26 @@ extern "C" int ebsdvae_in_bwd_apply_max(const float* gnext, int pmode, const flo
   return evh::check_launch("in_bwd_apply");
 }
 
+// the apply of a block whose output gradient came from a fused input-gradient conv, which
+// writes h = g * lrelu'(xhat) (conv_common.h): the same pass without the LeakyReLU factor
+extern "C" int ebsdvae_in_bwd_happly(const float* h, int pmode, const float* y, const float* stats,
+                                     const float* bstats, float* gy, float* gmax, int B, int H,
+                                     int W, int C, ebsdvae_stream_t stream) {
+  EV_REQUIRE(h && y && stats && bstats && gy, "in_bwd_happly: null pointer");
+  EV_REQUIRE(pmode >= 0 && pmode <= 2 && C % 4 == 0 && (256 % (C / 4)) == 0, "in_bwd_happly: bad pmode/C");
+  const int T = in_bwd_apply_tiles_host(B, H, W);
+  if (hipEvent_t fe = evh::take_fork_event()) {
+    hipExtLaunchKernelGGL((in_bwd_kernel<true, true>), dim3(T, B), dim3(256), 0, (hipStream_t)stream,
+                          nullptr, fe, 0, h, pmode, y, (const float2*)stats, (const float2*)bstats,
+                          (double2*)nullptr, gy, H, W, C, T, gmax);
+  } else {
+    hipLaunchKernelGGL((in_bwd_kernel<true, true>), dim3(T, B), dim3(256), 0, (hipStream_t)stream, h,
+                       pmode, y, (const float2*)stats, (const float2*)bstats, (double2*)nullptr, gy,
+                       H, W, C, T, gmax);
+  }
+  return evh::check_launch("in_bwd_happly");
+}
+
 extern "C" int ebsdvae_in_bwd_apply(const float* gnext, int pmode, const float* y,
                                     const float* stats, const float* bstats, float* gy, int B,
                                     int H, int W, int C, ebsdvae_stream_t stream) {
@@ -669,6 +692,38 @@ extern "C" int ebsdvae_in_bwd_first_apply_wgrad_rc(const float* gnext, const flo
                      (const float2*)stats, (const float2*)bstats, x, (double2*)nullptr, wpart, bpart,
                      (float*)nullptr, H, W, T, (float*)nullptr, b0);
   return evh::check_launch("in_bwd_first_apply_wgrad_rc");
+}
+
+// the first block's pass with h (a fused input gradient's output) instead of g
+extern "C" int ebsdvae_in_bwd_first_happly_wgrad_rc(const float* h, const float* w0, const float* b0,
+                                                    const float* stats, const float* bstats,
+                                                    const float* x, float* wpart, float* bpart,
+                                                    int B, int H, int W, int C,
+                                                    ebsdvae_stream_t stream) {
+  EV_REQUIRE(h && w0 && stats && bstats && x && wpart && bpart && C == 32,
+             "in_bwd_first_happly_wgrad_rc: bad args (C must be 32)");
+  const int T = in_bwd_tiles_host(H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST_RC, true, true>), dim3(T, B), dim3(256),
+                     edge_lds(H, W, T), (hipStream_t)stream, h, w0, (const float*)nullptr,
+                     (const float2*)stats, (const float2*)bstats, x, (double2*)nullptr, wpart, bpart,
+                     (float*)nullptr, H, W, T, (float*)nullptr, b0);
+  return evh::check_launch("in_bwd_first_happly_wgrad_rc");
+}
+
+extern "C" int ebsdvae_in_bwd_first_happly_wgrad(const float* h, const float* y, const float* stats,
+                                                 const float* bstats, const float* x, float* wpart,
+                                                 float* bpart, int B, int H, int W, int C,
+                                                 ebsdvae_stream_t stream) {
+  EV_REQUIRE(h && y && stats && bstats && x && wpart && bpart && C == 32,
+             "in_bwd_first_happly_wgrad: bad args (C must be 32)");
+  const int T = in_bwd_tiles_host(H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
+                     (hipStream_t)stream, h, (const float*)nullptr, y, (const float2*)stats,
+                     (const float2*)bstats, x, (double2*)nullptr, wpart, bpart, (float*)nullptr, H, W,
+                     T, (float*)nullptr);
+  return evh::check_launch("in_bwd_first_happly_wgrad");
 }
 
 extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float* y,

@@ -31,6 +31,8 @@ SIGNATURES = {
     "ebsdvae_conv_first_stat_tiles": [I, I],
     "ebsdvae_conv_first_fwd": [P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_apply_wgrad_rc": [P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_first_happly_wgrad_rc": [P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_first_happly_wgrad": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_pack_conv_weight": [P, P, I, I, I, I, P],
     "ebsdvae_pack_conv_weights": [P, I, P],
     "ebsdvae_conv3x3_fwd": [P, P, I, P, P, P, P, P, I, I, I, I, I, P],
@@ -66,6 +68,7 @@ SIGNATURES = {
     "ebsdvae_in_bwd_apply": [P, I, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_apply_tiles": [I, I, I, I],
     "ebsdvae_in_bwd_apply_max": [P, I, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_in_bwd_happly": [P, I, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_upsample2_bwd": [P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_final_reduce": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_final_apply": [P, P, P, P, P, P, I, I, I, I, P],
@@ -127,6 +130,7 @@ class WgradReduceDesc(ctypes.Structure):
 
 
 MAX_WGRAD_BATCH = 32
+
 
 
 class NativeLibraryError(RuntimeError):

@@ -496,9 +496,11 @@ def conv_forward(src, src_stats, layer: ConvLayer, w, b, B, keep_act=False, wp=N
 def in_backward(gnext, pmode, y, st, part=None):
     """gy = d loss / d y through [pool|up] . lrelu . InstanceNorm of one block.
     part: the reduce-pass sums already produced by the fused input-gradient conv that
-    computed gnext (conv_dgrad(..., prev=...)); None runs the reduce pass here."""
+    computed gnext (conv_dgrad(..., prev=...)), which then holds h = g * lrelu'(xhat), not g
+    (csrc/conv_common.h); None: gnext is g and the reduce pass runs here."""
     B, H, W, C = y.shape
     s = N.stream()
+    hin = part is not None
     if part is None:
         T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
         part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
@@ -513,9 +515,12 @@ def in_backward(gnext, pmode, y, st, part=None):
         # per-tile max |gy|: the scale of the split-fp16 input-gradient conv that consumes gy
         Tg = N.call("ebsdvae_in_bwd_apply_tiles", B, H, W, C)
         gmax = _empty(B, Tg, like=y)
-        N.call("ebsdvae_in_bwd_apply_max", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
-               N.ptr(gy), N.ptr(gmax), B, H, W, C, s)
+        N.call("ebsdvae_in_bwd_happly" if hin else "ebsdvae_in_bwd_apply_max", N.ptr(gnext), pmode,
+               N.ptr(y), N.ptr(st), N.ptr(bst), N.ptr(gy), N.ptr(gmax), B, H, W, C, s)
         gy.ev_gmax = gmax
+    elif hin:
+        N.call("ebsdvae_in_bwd_happly", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
+               N.ptr(gy), None, B, H, W, C, s)
     else:
         N.call("ebsdvae_in_bwd_apply", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), N.ptr(bst),
                N.ptr(gy), B, H, W, C, s)
@@ -824,6 +829,7 @@ def in_backward_first(gnext, y, st, x, dw0, db0, part=None, w0=None, b0=None):
     w0, b0: the first conv's parameters; with them, and y from ebsdvae_conv_first_fwd, y is
     recomputed from x instead of read."""
     B, H, W, C = y.shape
+    hin = part is not None   # gnext is a fused input gradient's h (see in_backward)
     if part is None:
         T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
         part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
@@ -835,11 +841,13 @@ def in_backward_first(gnext, y, st, x, dw0, db0, part=None, w0=None, b0=None):
     wpart = _empty(S_, 9, C, 1, like=y)
     bpart = _empty(S_, C, like=y)
     if w0 is not None and getattr(y, "ev_first_valu", False):
-        N.call("ebsdvae_in_bwd_first_apply_wgrad_rc", N.ptr(gnext), N.ptr(w0), N.ptr(b0), N.ptr(st),
-               N.ptr(bst), N.ptr(x), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
+        N.call("ebsdvae_in_bwd_first_happly_wgrad_rc" if hin else "ebsdvae_in_bwd_first_apply_wgrad_rc",
+               N.ptr(gnext), N.ptr(w0), N.ptr(b0), N.ptr(st), N.ptr(bst), N.ptr(x), N.ptr(wpart),
+               N.ptr(bpart), B, H, W, C, N.stream())
     else:
-        N.call("ebsdvae_in_bwd_first_apply_wgrad", N.ptr(gnext), N.ptr(y), N.ptr(st), N.ptr(bst),
-               N.ptr(x), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
+        N.call("ebsdvae_in_bwd_first_happly_wgrad" if hin else "ebsdvae_in_bwd_first_apply_wgrad",
+               N.ptr(gnext), N.ptr(y), N.ptr(st), N.ptr(bst), N.ptr(x), N.ptr(wpart), N.ptr(bpart),
+               B, H, W, C, N.stream())
     _reduce_slices(wpart, bpart, S_, 1, C, KIND_CONV, dw0, db0)
 
 
@@ -909,7 +917,8 @@ def _conv_wgrad(src, src_stats, src_mode, gy, cin, cout, kind, dw, db, normalize
 def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False, ypool=None):
     """Input gradient of `layer`.  prev = (y_prev, st_prev, pmode_prev) of the block feeding
     it: the previous block's InstanceNorm-backward reduce is then fused into the epilogue and
-    (gin, part) is returned for in_backward(..., part=part).
+    (gin, part) is returned for in_backward(..., part=part); gin is then h = g * lrelu'(xhat),
+    not g (csrc/conv_common.h).
     sum_up (pmode_prev == P_UP): where the split kernel supports it, gin is returned already
     2x2-summed, i.e. at the previous block's resolution (then in_backward takes it as P_ID).
     ypool (pmode_prev == P_POOL): the previous block's max-pooled raw output, which its forward

@@ -85,14 +85,18 @@ int ebsdvae_conv3x3_fwd(const float* src, const float* src_stats, int src_mode,
 int ebsdvae_conv3x3_stat_tiles(int H, int W, int cout);
 
 /* Input gradient of a conv (ebsdvae_conv3x3_fwd with a for_dgrad pack and RAW source:
- * gin = d loss / d a_prev at (B,H,W,cout) NHWC) fused with the reduce pass of the
- * PREVIOUS block's InstanceNorm backward (ebsdvae_in_bwd_reduce(gin, pmode, y_prev,
+ * g = d loss / d a_prev at (B,H,W,cout) NHWC) fused with the reduce pass of the
+ * PREVIOUS block's InstanceNorm backward (ebsdvae_in_bwd_reduce(g, pmode, y_prev,
  * st_prev, ...)).  a_prev = pmode(lrelu(IN(y_prev))); y_prev is (B,2H,2W,cout) for P_POOL,
  * (B,H/2,W/2,cout) for P_UP, (B,H,W,cout) for P_ID.  part receives double2
- * {sum g_a, sum g_a*xhat} per (b, tile, c) with ebsdvae_conv3x3_stat_tiles(H,W,cout) tiles
+ * {sum h, sum h*xhat} per (b, tile, c) with ebsdvae_conv3x3_stat_tiles(H,W,cout) tiles
  * per image; ebsdvae_in_bwd_finalize(part, ..., tiles, HW of y_prev) turns them into the
- * apply-pass statistics.  Replaces autograd's conv input gradient plus the first half of
- * the InstanceNorm backward (latice/model.py:95-97,102-106).  W must be a power of two. */
+ * apply-pass statistics.  gin receives h = g * lrelu'(xhat), xhat that of the y_prev pixel g
+ * routes to (the first 2x2 argmax for P_POOL, the parent for P_UP): the operand of
+ * ebsdvae_in_bwd_happly / _first_happly_wgrad*, which need no LeakyReLU branch of their own.
+ * Every fused input-gradient entry point below (pmode >= 0) writes h the same way.
+ * Replaces autograd's conv input gradient plus the first half of the InstanceNorm backward
+ * (latice/model.py:95-97,102-106).  W must be a power of two. */
 int ebsdvae_conv3x3_dgrad_inbwd(const float* g, const float* wpack, float* gin,
                                 const float* y_prev, const float* st_prev, int pmode,
                                 double* part, int B, int H, int W, int cin, int cout,
@@ -277,6 +281,11 @@ int ebsdvae_in_bwd_apply_tiles(int B, int H, int W, int C);
 int ebsdvae_in_bwd_apply_max(const float* gnext, int pmode, const float* y, const float* stats,
                              const float* bstats, float* gy, float* gmax, int B, int H, int W,
                              int C, ebsdvae_stream_t stream);
+/* As ebsdvae_in_bwd_apply_max for h (a fused input gradient's output, routed like gnext):
+ * the LeakyReLU factor is already in it.  gmax may be NULL. */
+int ebsdvae_in_bwd_happly(const float* h, int pmode, const float* y, const float* stats,
+                          const float* bstats, float* gy, float* gmax, int B, int H, int W, int C,
+                          ebsdvae_stream_t stream);
 /* Network-end fusions (C == 32; slices = B * ebsdvae_in_bwd_tiles(H,W,C) partials for
  * ebsdvae_wgrad_reduce):
  *  final_*: the block feeding the last conv (latice/model.py:147-148).  Its output gradient
@@ -310,6 +319,15 @@ int ebsdvae_in_bwd_first_apply_wgrad_rc(const float* gnext, const float* w0, con
                                         const float* stats, const float* bstats, const float* x,
                                         float* wpart, float* bpart, int B, int H, int W, int C,
                                         ebsdvae_stream_t stream);
+/* The first block's pass (the two above) on h, a fused input gradient's output */
+int ebsdvae_in_bwd_first_happly_wgrad(const float* h, const float* y, const float* stats,
+                                      const float* bstats, const float* x, float* wpart,
+                                      float* bpart, int B, int H, int W, int C,
+                                      ebsdvae_stream_t stream);
+int ebsdvae_in_bwd_first_happly_wgrad_rc(const float* h, const float* w0, const float* b0,
+                                         const float* stats, const float* bstats, const float* x,
+                                         float* wpart, float* bpart, int B, int H, int W, int C,
+                                         ebsdvae_stream_t stream);
 /* gradient of nearest x2 upsampling: out[b,h,w,c] = sum of the 2x2 block of g (at 2H) */
 int ebsdvae_upsample2_bwd(const float* g, float* out, int B, int H, int W, int C,
                           ebsdvae_stream_t stream);

@@ -166,6 +166,20 @@ def test_instance_norm_backward(cuda, pmode, H, C):
     assert O.rel_err(host(gy), ref) < 1e-4
 
 
+def h_oracle(gn, xh, pmode, summed=False):
+    """What a fused input gradient writes (csrc/conv_common.h): h = g * lrelu'(xhat) at the
+    y_prev pixel g routes to -- pooled resolution for P_POOL (xhat at the window maximum),
+    the consumer's resolution for P_UP (the parent's xhat), y_prev's for the summed upsample
+    adjoint (summed=True: the 2x2 sums of g)."""
+    if pmode == E.P_POOL:
+        return gn * O.lrelu_slope(O.maxpool2(xh)[0])
+    if pmode == E.P_UP and not summed:
+        return gn * O.lrelu_slope(O.upsample2(xh))
+    if summed:
+        gn = O.upsample2_bwd(gn)
+    return gn * O.lrelu_slope(xh)
+
+
 FUSED_CASES = [  # (layer cin, layer cout, H, pmode of the block feeding the layer)
     (32, 32, 128, E.P_ID), (32, 64, 64, E.P_POOL), (64, 128, 32, E.P_POOL), (128, 128, 16, E.P_UP),
     (128, 128, 8, E.P_POOL), (128, 128, 8, E.P_ID), (64, 32, 64, E.P_UP), (128, 64, 32, E.P_ID),
@@ -189,7 +203,7 @@ def test_dgrad_fused_instance_norm_backward(cuda, cin, cout, H, pmode):
     gin, part = E.conv_dgrad(dev(gy), layer, dev(wsrc), prev=(y_d, st_d, pmode))
     g_prev = E.in_backward(gin, pmode, y_d, st_d, part=part)
     gn = O.conv3x3_dgrad(gy, wsrc)
-    assert O.rel_err(host(gin), gn) < TOL
+    assert O.rel_err(host(gin), h_oracle(gn, xh, pmode)) < TOL
     a = O.lrelu(xh)
     if pmode == E.P_POOL:
         _, arg = O.maxpool2(a)
@@ -562,7 +576,7 @@ def test_dgrad_fused_split_bf16(cuda, cin, cout, H, pmode, prec):
     finally:
         E.set_precision(old)
     gn = O.conv3x3_dgrad(gy, wsrc)
-    assert O.rel_err(host(gin), gn) < SPLIT_TOL[prec]
+    assert O.rel_err(host(gin), h_oracle(gn, xh, pmode)) < SPLIT_TOL[prec]
     assert O.rel_err(host(gin2), gn) < SPLIT_TOL[prec]
     a = O.lrelu(xh)
     if pmode == E.P_POOL:
@@ -615,8 +629,9 @@ def test_dgrad_fused_split_f16(cuda, cin, cout, H, pmode, gscale, wscale):
         gin2 = E.conv_dgrad(g_d, layer, w_d, wd=wd)
         gmax = host(g_prev.ev_gmax)
     gn = O.conv3x3_dgrad(gy, wsrc)
+    hn = h_oracle(gn, xh, pmode)
     for b in range(B):   # per image: the two differ by 1e3 in magnitude
-        assert O.rel_err(host(gin)[b], gn[b]) < SPLIT_TOL["f16x3"], b
+        assert O.rel_err(host(gin)[b], hn[b]) < SPLIT_TOL["f16x3"], b
         assert O.rel_err(host(gin2)[b], gn[b]) < SPLIT_TOL["f16x3"], b
     a = O.lrelu(xh)
     if pmode == E.P_POOL:
@@ -748,7 +763,7 @@ def test_dgrad_summed_upsample_adjoint(cuda, cin, cout, H, prec):
         g_prev2 = E.in_backward(gin, E.P_UP, y_d, st_d, part=part2)
     gn = O.conv3x3_dgrad(gy, wsrc)
     ga = O.upsample2_bwd(gn)
-    assert O.rel_err(host(gsum), ga) < SPLIT_TOL[prec]
+    assert O.rel_err(host(gsum), h_oracle(gn, xh, E.P_UP, summed=True)) < SPLIT_TOL[prec]
     ref = O.instance_norm_bwd(ga * O.lrelu_slope(xh), xh, rstd)
     assert O.rel_err(host(g_prev), ref) < 2e-4
     assert O.rel_err(host(g_prev), host(g_prev2)) < 2e-4
@@ -965,3 +980,4 @@ def test_network_end_matches_oracle(cuda):
     ref = O.vae_loss(ref_xhat[:, None], x, z, mu, sd, 5e-6)
     assert abs(float(loss) - ref["loss"]) <= 1e-5 * abs(ref["loss"])
     assert O.rel_err(host(elbo), ref["elbo"]) < 1e-5
+
