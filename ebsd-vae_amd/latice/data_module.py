@@ -222,12 +222,21 @@ class DeviceBatchLoader:
         it, else 0), padded by wrapping to a multiple of W, then every W-th index from the
         rank's offset -- so the ranks see disjoint batches that cover the epoch.
         `set_epoch(e)` (reached through `.sampler`, where Lightning looks for it) moves to
-        epoch e."""
+        epoch e.
+    Every torch DataLoader iterator draws a base seed from the default generator when it is
+    created -- in order or shuffled, one process or W ranks -- except that a loader with
+    persistent workers (the reference's val/test loaders when n_cpu > 0) creates its
+    iterator once and draws it on the first iteration only; `persistent` says which.  Both
+    draws (base seed, then RandomSampler's) happen when iter() is called, as DataLoader's
+    worker iterator prefetches at creation, so later epochs and the other loaders see the
+    reference's generator state."""
 
     def __init__(self, dataset: DPdataset, indices, batch_size: int, shuffle: bool = False,
                  drop_last: bool = False, rank: int | None = None, world: int | None = None,
-                 seed: int | None = None):
+                 seed: int | None = None, persistent: bool = False):
         self.dataset = dataset
+        self.persistent = bool(persistent)
+        self._iterated = False
         self.indices = np.asarray(indices, dtype=np.int64)
         self.batch_size = int(batch_size)
         self.shuffle = bool(shuffle)
@@ -261,6 +270,9 @@ class DeviceBatchLoader:
 
     def _order(self):
         n = len(self.indices)
+        if not (self.persistent and self._iterated):
+            torch.empty((), dtype=torch.int64).random_()   # the iterator's base seed
+        self._iterated = True
         if self.world > 1:
             # torch.utils.data.DistributedSampler (shuffle, drop_last=False)
             if self.shuffle:
@@ -275,15 +287,17 @@ class DeviceBatchLoader:
             return self.indices[pos[self.rank:total:self.world]]
         if not self.shuffle:
             return self.indices
-        # DataLoader.__iter__ draws its base seed, then RandomSampler.__iter__ its own seed
-        torch.empty((), dtype=torch.int64).random_()
+        # after the base seed, RandomSampler.__iter__ draws its own seed
         seed = int(torch.empty((), dtype=torch.int64).random_().item())
         g = torch.Generator()
         g.manual_seed(seed)
         return self.indices[torch.randperm(n, generator=g).numpy()]
 
     def __iter__(self):
-        order = self._order()
+        # the generator draws happen here, at iter(), not at the first next()
+        return self._batches(self._order())
+
+    def _batches(self, order):
         nb = len(self)
         if nb == 0:
             return
@@ -330,8 +344,9 @@ class DeviceBatchLoader:
 
 class DPDataModule(_DMBase):
     """data_module.py:136-261: same arguments, split and loaders; the loaders yield device
-    batches (DeviceBatchLoader).  `n_cpu` is accepted for API compatibility: there are no
-    worker processes (one transform launch per batch replaces them)."""
+    batches (DeviceBatchLoader).  `n_cpu` starts no worker processes (one transform launch
+    per batch replaces them); it only decides, as in the reference, whether the val/test
+    loaders are persistent, which changes their generator draws."""
 
     def __init__(self, path, rot_angles_path, image_size=(128, 128), val_data_ratio: float = 0.1,
                  batch_size: int = 32, n_cpu: int = 4, seed: int = 42, transform=None,
@@ -366,7 +381,9 @@ class DPDataModule(_DMBase):
 
     def _loader(self, subset, shuffle):
         idx = subset.indices if hasattr(subset, "indices") else np.arange(len(subset))
-        return DeviceBatchLoader(self.dataset_full, idx, self.batch_size, shuffle=shuffle)
+        # val/test: persistent_workers=n_cpu > 0 (data_module.py:245,260)
+        return DeviceBatchLoader(self.dataset_full, idx, self.batch_size, shuffle=shuffle,
+                                 persistent=not shuffle and self.n_cpu > 0)
 
     def train_dataloader(self) -> DeviceBatchLoader:
         """data_module.py:215-233 (with no validation split, the whole set)."""

@@ -92,3 +92,32 @@ def test_two_rank_group_gives_disjoint_batches():
     assert [res[r][:2] for r in range(world)] == [(0, 2), (1, 2)]
     a, b = res[0][2], res[1][2]
     assert not set(a) & set(b) and sorted(a + b) == list(range(64))
+
+
+@pytest.mark.parametrize("n_cpu", [0, 1])
+def test_val_then_train_follow_reference_generator(n_cpu):
+    """Lightning's fit: a sanity-check pass over the val loader, then per epoch the train
+    loader and the val loader.  Every DataLoader iterator draws a base seed, the persistent
+    val loader (n_cpu > 0) only on its first iteration (data_module.py:225-246)."""
+    n_tr, n_va, bs, seed = 37, 11, 8, 3
+    torch.manual_seed(seed)
+    tr = DataLoader(TensorDataset(torch.arange(n_tr)), batch_size=bs, shuffle=True, num_workers=n_cpu)
+    va = DataLoader(TensorDataset(torch.arange(n_va)), batch_size=bs, shuffle=False,
+                    num_workers=n_cpu, persistent_workers=n_cpu > 0)
+    ref = [[b[0].tolist() for b in va]]
+    for _ in range(2):
+        ref.append([b[0].tolist() for b in tr])
+        ref.append([b[0].tolist() for b in va])
+    ref_next = torch.rand(3)
+    del tr, va
+
+    torch.manual_seed(seed)
+    mtr = DeviceBatchLoader(None, np.arange(n_tr), bs, shuffle=True, rank=0, world=1)
+    mva = DeviceBatchLoader(None, np.arange(n_va), bs, shuffle=False, rank=0, world=1,
+                            persistent=n_cpu > 0)
+    got = [_mine(mva)]
+    for _ in range(2):
+        got.append(_mine(mtr))
+        got.append(_mine(mva))
+    assert got == ref
+    assert torch.equal(torch.rand(3), ref_next)     # the generator ends in the same state
