@@ -153,6 +153,17 @@ EV_DEVINL void split_f16x2(float a, float b, unsigned& hi, unsigned& lo) {
       "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
       : "=&v"(lo) : "v"(hi), "v"(a), "v"(b));
 }
+// split_f16x2 of (a * s, b * s) for a power of two s (the gradient operands' scale): the
+// products are exact in fp32, so hi = f16(a s) by one v_fma_mix (a s + 0) and lo = f16(a s - hi)
+// by another (fma_mix forms a s - hi exactly and rounds once) -- the same bits as scaling first
+// and splitting, in 4 instructions instead of 5
+EV_DEVINL void split_f16x2_scaled(float a, float b, float s, unsigned& hi, unsigned& lo) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi), "=&v"(lo) : "v"(a), "v"(b), "v"(s));
+}
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // k such that m * 2^k lies in [2^11, 2^12) (0 for a zero / non-finite maximum)

@@ -43,10 +43,15 @@ EV_DEVINL int inbwd_pix(int pl, int W, int lW, int k) {
   return (2 * h + (k >> 1)) * (2 * W) + 2 * w + (k & 1);   // P_POOL window (k = dy*2+dx)
 }
 
+// sp = {mean, rstd} of the y_prev channel; c = -mean * rstd.  Identity / upsample routing: the
+// LeakyReLU branch is y > mean -- exactly the sign of (y - mean) * rstd (rstd > 0, no
+// underflow), which the pinned oracle evaluates -- and xhat, which only enters the second sum,
+// is one fma.  The 2x2 argmax compares lrelu((y - mean) * rstd) as the reference's pool does.
 template <int FP>
-EV_DEVINL float inbwd_acc(float g, const float* v, float2 sp, float& s1, float& s2) {
-  float x = (v[0] - sp.x) * sp.y;
+EV_DEVINL float inbwd_acc(float g, const float* v, float2 sp, float c, float& s1, float& s2) {
+  float ga, x;
   if (FP == P_POOL) {   // first maximum of lrelu(xhat) in window order (0,0),(0,1),(1,0),(1,1)
+    x = (v[0] - sp.x) * sp.y;
     float best = lrelu(x);
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
@@ -54,8 +59,11 @@ EV_DEVINL float inbwd_acc(float g, const float* v, float2 sp, float& s1, float& 
       const float f = lrelu(xk);
       if (f > best) { best = f; x = xk; }
     }
+    ga = g * slope(x);
+  } else {
+    x = fmaf(v[0], sp.y, c);
+    ga = v[0] > sp.x ? g : g * kSlope;
   }
-  const float ga = g * slope(x);
   s1 += ga;
   s2 = fmaf(ga, x, s2);
   return ga;
@@ -99,6 +107,7 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
       const size_t plane = FP == P_POOL ? (size_t)4 * H * W : (FP == P_UP ? (size_t)(H * W) / 4 : (size_t)H * W);
       const float* yp = yprev + (size_t)gb * plane * Cout + co;
       const float2 sp = stprev[(size_t)gb * Cout + co];
+      const float sc = -sp.x * sp.y;
       const int pbase = h0 * W - wimg * tpx + wpx0 + 4 * hk;
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -114,7 +123,7 @@ EV_DEVINL void conv_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 #pragma unroll
         for (int j = 0; j < G; ++j) {
           const int e = e0 + j, mf = e >> 4, r = e & 15;
-          const float h = inbwd_acc<FP>(acc[mf][nf][r], v[j], sp, s1, s2);
+          const float h = inbwd_acc<FP>(acc[mf][nf][r], v[j], sp, sc, s1, s2);
           const int rem = wpx0 + mf * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk - wimg * tpx;
           y[(((size_t)gb * H + h0) * W + rem) * Cout + co] = h;
         }

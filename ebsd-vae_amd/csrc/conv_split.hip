@@ -104,6 +104,16 @@ EV_DEVINL void split4(float4 v, bf16x4 (&out)[npc(NP)]) {
 }
 
 // one 32x32x16 product of two piece fragments (bf16, or fp16 bits for NP_F16)
+// split4 of v * s (s a power of two) for the fp16 pieces: split_f16x2_scaled
+EV_DEVINL void split4_f16_scaled(float4 v, float s, bf16x4 (&out)[2]) {
+  unsigned h01, l01, h23, l23;
+  split_f16x2_scaled(v.x, v.y, s, h01, l01);
+  split_f16x2_scaled(v.z, v.w, s, h23, l23);
+  typedef unsigned u2 __attribute__((ext_vector_type(2)));
+  out[0] = __builtin_bit_cast(bf16x4, u2{h01, h23});
+  out[1] = __builtin_bit_cast(bf16x4, u2{l01, l23});
+}
+
 template <int NP>
 EV_DEVINL f32x16 mfma_piece(bf16x8 a, bf16x8 b, f32x16 c) {
   if constexpr (NP == NP_F16)
@@ -444,11 +454,21 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         const float v = fmaf(acc[mf][nf][r], sc, bb);
         acc[mf][nf][r] = v;
         if constexpr (!FUSED) s[mf >> 1] += v;   // input-gradient convs write no statistics
-        // fused input gradients write h (below); pooled inference writes ypool only
-        if (!FUSED && (FP != FP_POOLOUT || y))
+      }
+    // fused input gradients write h (below); pooled inference writes ypool only (one uniform
+    // branch, not one per value)
+    if (!FUSED && (FP != FP_POOLOUT || y)) {
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          // (a named float: __builtin_bit_cast of the vector-element lvalue itself reads
+          // element 0 -- hipcc / ROCm 7.2)
+          const float v = acc[mf][nf][r];
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
                                                 vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
-      }
+        }
+    }
     if (FP == FP_UPSUM) {
       // y is (B, H/2, W/2, NT): the 2x2 sums of this conv's output (the upsample adjoint),
       // and the previous block (at H/2) is reduced once per window:
@@ -459,6 +479,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
       const auto rp = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(yprev + ((size_t)b0 * (H >> 1) + (h0 >> 1)) * W2 * NT), 0, 0x7fffffff, 0x00020000);
       const float2 sp = stprev[(size_t)b0 * NT + co];
+      const float spc = -sp.x * sp.y;
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
         const int m0 = 2 * g;   // the group's fragment pair
@@ -487,7 +508,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float h = inbwd_acc<P_ID>(gs[k], &v[k], sp, s1, s2);
+          const float h = inbwd_acc<P_ID>(gs[k], &v[k], sp, spc, s1, s2);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), rq, off[k], 0, 0);
         }
         s1 += __shfl_xor(s1, 32, 64);
@@ -539,6 +560,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
       const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)(yprev + (size_t)b0 * plane * NT), 0,
                                                         plane * NT * 4, 0x00020000);
       const float2 sp = stprev[(size_t)b0 * NT + co];
+      const float spc = -sp.x * sp.y;
       const int pbase = h0 * W + wpx0 + 4 * hk;
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
@@ -559,7 +581,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 #pragma unroll
           for (int j = 0; j < G; ++j) {
             const int e = e0 + j, mf = e >> 4, r = e & 15;
-            const float h = inbwd_acc<FP>(acc[mf][nf][r], v[j], sp, s1, s2);
+            const float h = inbwd_acc<FP>(acc[mf][nf][r], v[j], sp, spc, s1, s2);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), ry,
                                                   vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
           }
@@ -629,7 +651,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr int NR = POOL ? 4 : 1;
   constexpr bool GS = (NP == NP_F16 && MODE == ACT_RAW);   // per-image gradient scale
   constexpr int PD = POOL ? 1 : 2;               // halo prefetch distance (iterations)
-  static_assert(PD == 1 || KX * NR <= 7, "pipe_barrier keeps at most 7 loads in flight");
+  // vector-memory ops issue_halo makes per iteration: the halo loads and, for NORM sources, the
+  // two per-lane loads of the chunk's statistics (the barrier leaves exactly these in flight)
+  constexpr int NLD = KX * NR + (NORM ? 2 : 0);
+  static_assert(PD == 1 || NLD <= 15, "pipe_barrier: vmcnt range");
   static_assert(WR == 0 || (PD == 2 && NI == 1), "resident weights: single-image, prefetch 2");
   extern __shared__ __attribute__((aligned(16))) char xsm[];
   // a tile is TH rows of one image, or NI whole images (NI > 1: TH == H); NI is a template
@@ -779,14 +804,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
       }
     }
     if (NORM) {
-      // the chunk's 8 {mean, rstd} pairs are wave-uniform: one scalar-cache load (no TA
-      // traffic), then each lane keeps its 4-channel half
+      // each lane loads the {mean, rstd} of its own 4-channel half (two 16-byte vector loads;
+      // a wave-uniform scalar load would need 3 VALU per value to hand each lane its half)
       const int bs = NI == 1 ? b0 : min(b0 + img_u, B - 1);   // this wave's image
-      const float4* sp = reinterpret_cast<const float4*>(sstats + (size_t)bs * Cin + ch * XCK);
-      const float4 u0 = sp[0], u1 = sp[1], u2 = sp[2], u3 = sp[3];
-      const float4 s01 = q ? u2 : u0, s23 = q ? u3 : u1;
-      st[sl][0] = make_float2(s01.x, s01.y); st[sl][1] = make_float2(s01.z, s01.w);
-      st[sl][2] = make_float2(s23.x, s23.y); st[sl][3] = make_float2(s23.z, s23.w);
+      const float4* sp = reinterpret_cast<const float4*>(sstats + (size_t)bs * Cin + ch * XCK + q * 4);
+      const float4 u0 = sp[0], u1 = sp[1];
+      st[sl][0] = make_float2(u0.x, u0.y); st[sl][1] = make_float2(u0.z, u0.w);
+      st[sl][2] = make_float2(u1.x, u1.y); st[sl][3] = make_float2(u1.z, u1.w);
     }
   };
   // transform + split item k of register slot sl into the LDS halo buffer lx
@@ -807,9 +831,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   auto stage_item = [&](auto slot_c, int k, const float2 (&fs)[4], char* lx) EV_LAMBDA_INLINE {
     constexpr int sl = decltype(slot_c)::value;
     float4 v = stage_value(slot_c, k, fs);
-    if constexpr (GS) v = make_float4(v.x * gsc[sl], v.y * gsc[sl], v.z * gsc[sl], v.w * gsc[sl]);
     bf16x4 pc[NPC];
-    split4<NP>(v, pc);
+    if constexpr (GS)   // the per-image gradient scale folded into the split
+      split4_f16_scaled(v, gsc[sl], pc);
+    else
+      split4<NP>(v, pc);
     char* d = lx + ldo[k];
 #pragma unroll
     for (int i = 0; i < NPC; ++i) *reinterpret_cast<bf16x4*>(d + 16 * i) = pc[i];
@@ -1051,7 +1077,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
       if constexpr (WR > 0)
         pipe_barrier_lds();
       else
-        pipe_barrier<(PD == 2 ? KX * NR : 0)>();
+        pipe_barrier<(PD == 2 ? NLD : 0)>();
     } else {
 #ifndef EV_PIPE_NOBAR
       __syncthreads();
@@ -1099,7 +1125,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   }
   if constexpr (WR) {
     // the resident slabs are older than both halo loads: all but the youngest (it 1's) landed
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KX * NR) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD) : "memory");
   }
   __syncthreads();
   // nch = Cin / 8 is even for every supported layer (plan_split), so it & 1 == ch & 1

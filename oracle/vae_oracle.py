@@ -200,7 +200,8 @@ def pinned_routing(y, st, pool: bool):
     """The discrete backward decisions of one block, taken from a float32 run's saved
     pre-norm output y (B,H,W,C) and statistics st (B,C,2) = {mean, rstd}, evaluated exactly
     as the HIP backward evaluates them (csrc/instnorm.hip in_bwd_kernel, conv_common.h
-    inbwd_acc): xhat = (y - mean) * rstd in float32, LeakyReLU slope 1 where xhat > 0, and
+    inbwd_acc): xhat = (y - mean) * rstd in float32, LeakyReLU slope 1 where xhat > 0 (the
+    fused reduce tests y > mean, the same predicate for rstd > 0), and
     for a max-pooled block the FIRST maximum of lrelu(xhat) = max(xhat, 0.02 xhat) in window
     order (0,0),(0,1),(1,0),(1,1) (ATen's CPU max_pool2d rule, latice/model.py:112-124).
 
