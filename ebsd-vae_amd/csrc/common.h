@@ -197,6 +197,9 @@ hipEvent_t take_fork_event();
 
 // a spatial extent the shape queries accept (H * W and its multiples stay inside int)
 inline bool ev_dim_ok(int n) { return n > 0 && n <= 65536 && (long long)n * n <= (1LL << 30); }
+// a per-image byte range the 32-bit buffer descriptors can address (num_records and the
+// offsets are 32-bit; out-of-range reads return 0, so an overflow would read zeros silently)
+inline bool ev_buf_bytes_ok(long long bytes) { return bytes > 0 && bytes < (1LL << 31); }
 
 #define EV_REQUIRE(cond, ...)        \
   do {                               \

@@ -1317,6 +1317,9 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
   // the pipelined kernel maps iterations to (image, row band, chunk) by shifts
   auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
   if (!pow2(cin / XCK) || !pow2(H) || !pow2(W)) return false;
+  // per-image byte ranges of the buffer descriptors (sources up to 2H x 2W for max-pool
+  // modes, outputs and the fused reduce's y_prev windows): 32-bit
+  if (!ev_buf_bytes_ok(4LL * H * W * (cin > cout ? cin : cout) * 4)) return false;
   c->M = (np != 2 && cout != 128) ? 512 : 256;
   c->NI = 1;
   c->NT = cout;

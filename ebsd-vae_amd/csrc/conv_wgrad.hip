@@ -118,6 +118,8 @@ static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
   if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0) return false;
   if (H % 8 || W % 8 || cin % 32 || !(cout == 32 || cout % 64 == 0)) return false;
   if (((H / 8) & (H / 8 - 1)) || ((W / 8) & (W / 8 - 1))) return false;   // tile_at shifts
+  // per-image byte ranges of the source / gradient buffer descriptors: 32-bit
+  if (!ev_buf_bytes_ok(4LL * H * W * (cin > cout ? cin : cout) * 4)) return false;
   g->TW = 8; g->TH = 8; g->NI = 1;
   g->ntx = W / 8; g->nty = H / 8;
   g->lTW = 3; g->ltpx = 6;

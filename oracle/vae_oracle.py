@@ -304,12 +304,15 @@ def blocks_from_cache(cache):
     return blocks("enc"), blocks("dec")
 
 
-def backward(cache, x_nchw, kl_lambda, g_loss: float = 1.0, pins=None):
+def backward(cache, x_nchw, kl_lambda, g_loss: float = 1.0, pins=None, absum=None):
     """Gradients of compute_loss(...)['loss'] w.r.t. every parameter (state_dict names).
 
     pins (optional): {("enc"|"dec", i): (pos, arg)} from pinned_routing -- the LeakyReLU
     branch and max-pool argmax of block i are taken from there instead of from this
-    evaluation's own float64 activations (decision-pinned oracle)."""
+    evaluation's own float64 activations (decision-pinned oracle).
+    absum (optional dict): filled with, per conv bias feeding an InstanceNorm (whose gradient
+    sum_{b,h,w} gy is analytically zero), A_c = sum_{b,h,w} |gy| per channel -- the scale of
+    an fp32 run's rounding residue on that zero (tests/pinned.py)."""
     pins = pins or {}
     p = cache["p"]
     grads = {}
@@ -332,6 +335,8 @@ def backward(cache, x_nchw, kl_lambda, g_loss: float = 1.0, pins=None):
         # conv weight (Co,Ci,kh,kw) = wT[ci,co,2-kh,2-kw]  =>  d wT = transpose/flip back
         grads[f"decoder.{idx}.0.weight"] = np.ascontiguousarray(dw.transpose(1, 0, 2, 3)[:, :, ::-1, ::-1])
         grads[f"decoder.{idx}.0.bias"] = db
+        if absum is not None:
+            absum[f"decoder.{idx}.0.bias"] = np.abs(gy).sum(axis=(0, 1, 2))
         ga = conv3x3_dgrad(gy, ent["w"])
         if i in UP_BEFORE:
             ga = upsample2_bwd(ga)
@@ -360,6 +365,8 @@ def backward(cache, x_nchw, kl_lambda, g_loss: float = 1.0, pins=None):
         gy = instance_norm_bwd(gxh, ent["xh"], ent["rstd"])
         dw, db = conv3x3_wgrad(ent["a_in"], gy)
         grads[f"encoder.{idx}.0.weight"], grads[f"encoder.{idx}.0.bias"] = dw, db
+        if absum is not None:
+            absum[f"encoder.{idx}.0.bias"] = np.abs(gy).sum(axis=(0, 1, 2))
         if i > 0:
             ga = conv3x3_dgrad(gy, ent["w"])
     return grads

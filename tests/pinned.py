@@ -15,8 +15,12 @@ Two comparisons per parameter gradient g (norm-wise max|d|/max|ref|):
                    4e-2 from float64 with identical routing; the HIP run 2e-4).
 Measured on MI355X (round 2): decision-pinned <= 2.2e-4, state-pinned <= 3.4e-5 over all
 fixtures and the fp32 / bf16x6 / f16x3 arithmetics.
-The 19 conv biases feeding an affine-free InstanceNorm have an analytically zero gradient:
-absolute gate 1e-6.
+The 19 conv biases feeding an affine-free InstanceNorm have an analytically zero gradient
+(sum_{b,h,w} gy = 0): what an fp32 run returns is the rounding residue of that cancellation,
+which scales with the magnitude of the summed terms, A_c = sum_{b,h,w} |gy| (the oracle's,
+vae_oracle.backward(absum=...)), not with the batch.  Gate: |g_c| <= ZERO_BIAS_K * 2^-24 * A_c
+per channel (the reference's own fp32 residue at B=256 is recorded in
+tests/golden/bias_noise_b256.npz by make_bias_noise.py).
 """
 import functools
 import os
@@ -31,7 +35,8 @@ ZERO_GRAD_BIAS = tuple(f"encoder.{i}.0.bias" for i in O.ENC_IDX) + tuple(
     f"decoder.{i}.0.bias" for i in O.DEC_IDX)
 DECISION_GATE = 1e-3
 STATE_GATE = 1e-4
-ZERO_BIAS_GATE = 1e-6
+ZERO_BIAS_K = 4096.0     # residue <= 2.4e-4 of sum |gy| (units of 2^-24 * A_c)
+U32 = 2.0 ** -24
 
 
 @functools.lru_cache(maxsize=4)
@@ -69,14 +74,16 @@ def check_grads(name, plan, rec, grads, label=""):
     _, cache_s, pins = O.forward_from_state(sd, f["x"], f["eps"], enc_b, dec_b)
     g_state = O.backward(cache_s, f["x"], kl, pins=pins)
     _, cache64 = oracle_fp64(name)
-    g_dec = O.backward(cache64, f["x"], kl, pins=pins)
+    absum = {}
+    g_dec = O.backward(cache64, f["x"], kl, pins=pins, absum=absum)
     rows, fails = [], []
     for n in g_state:
         g = host(grads[n])
         if n in ZERO_GRAD_BIAS:
-            a = float(np.abs(g).max())
+            # residue in units of 2^-24 * A_c, worst channel
+            a = float((np.abs(g) / (U32 * np.maximum(absum[n], 1e-300))).max())
             rows.append((n, a, None))
-            if a > ZERO_BIAS_GATE:
+            if a > ZERO_BIAS_K:
                 fails.append((n, "zero-bias", a))
             continue
         es, ed = O.rel_err(g, g_state[n]), O.rel_err(g, g_dec[n])
@@ -89,8 +96,8 @@ def check_grads(name, plan, rec, grads, label=""):
     worst_d = max(r[2] for r in rows if r[2] is not None)
     worst_b = max(r[1] for r in rows if r[2] is None)
     print(f"\n[{label} {name}] worst weight-grad err: state-pinned {worst_s:.2e}, "
-          f"decision-pinned {worst_d:.2e}; worst |zero-grad bias| {worst_b:.2e}")
+          f"decision-pinned {worst_d:.2e}; worst zero-grad bias residue {worst_b:.1f} x 2^-24 A")
     for n, a, b in rows:
-        print(f"    {n:22s} " + (f"|g| {a:.2e}" if b is None else f"state {a:.2e}  decision {b:.2e}"))
+        print(f"    {n:22s} " + (f"residue {a:.1f} x 2^-24 A" if b is None else f"state {a:.2e}  decision {b:.2e}"))
     assert not fails, fails
     return worst_s, worst_d

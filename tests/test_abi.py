@@ -53,6 +53,20 @@ def test_library_loads_and_binds():
     assert _native.call("ebsdvae_in_bwd_tiles", 128, 128, 32) == 16
 
 
+def test_planners_reject_byte_ranges_past_32_bits():
+    """The split conv and weight-gradient kernels address one image through 32-bit buffer
+    descriptors (reads past the range return 0): the planners refuse shapes whose per-image
+    byte range reaches 2^31 instead of computing zeros silently."""
+    _ensure_built()
+    from latice import _native
+    from latice.engine import PIECES_F16
+    for np_ in (2, 3, PIECES_F16):
+        assert _native.call("ebsdvae_conv3x3_split_supported", 128, 128, 32, 32, np_) == 1
+        assert _native.call("ebsdvae_conv3x3_split_supported", 2048, 2048, 128, 128, np_) == 0
+    assert _native.call("ebsdvae_conv3x3_wgrad_split_slices", 256, 128, 128, 32, 32, PIECES_F16) > 0
+    assert _native.call("ebsdvae_conv3x3_wgrad_split_slices", 1, 2048, 2048, 128, 128, PIECES_F16) < 0
+
+
 def test_invalid_shapes_report_errors_without_gpu():
     _ensure_built()
     from latice import _native

@@ -101,6 +101,26 @@ def test_deferred_tensor_computes_on_first_use_only():
         bad.sum()
 
 
+def test_weight_writer_leaves_stale_deferred_values_to_their_reader():
+    """engine.before_weights_write (run by every raw-pointer weight writer) computes the pending
+    deferred values; one that can no longer be computed raises where it is read, not in the
+    optimizer step that happened to flush it."""
+    from latice import engine as E
+    from latice.deferred import DeferredTensor
+
+    def stale():
+        raise RuntimeError("model parameters changed between model(x) and the first use")
+
+    good = DeferredTensor(lambda: torch.ones(2), (2,), torch.float32, torch.device("cpu"))
+    bad = DeferredTensor(stale, (2,), torch.float32, torch.device("cpu"))
+    E.defer_until_weights_change(bad)
+    E.defer_until_weights_change(good)
+    E.before_weights_write()            # does not raise
+    assert good.materialized and not bad.materialized and not E._PENDING
+    with pytest.raises(RuntimeError, match="parameters changed"):
+        bad.sum()
+
+
 def test_datamodule_split_matches_random_split(tmp_path):
     """DPDataModule.setup('fit') splits exactly like the reference's random_split with the
     seeded generator (latice/data_module.py:194-207); loaders report len() in batches."""

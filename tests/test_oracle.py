@@ -81,8 +81,29 @@ def test_pinned_oracle_isolates_the_backward_arithmetic(name):
     _, cs, pins = O.forward_from_state(sd, f["x"], f["eps"], *O.blocks_from_cache(c32))
     g_state = O.backward(cs, f["x"], kl, pins=pins)
     _, c64 = O.forward(sd, f["x"], f["eps"])
-    g_dec = O.backward(c64, f["x"], kl, pins=pins)
+    absum = {}
+    g_dec = O.backward(c64, f["x"], kl, pins=pins, absum=absum)
     weights = [n for n in g32 if n.endswith("weight")]
     assert max(O.rel_err(g32[n], g_state[n]) for n in weights) < 1e-4
     if name != "vae128_b2_edge":
         assert max(O.rel_err(g32[n], g_dec[n]) for n in weights) < 2e-4
+    # the analytically-zero biases: an fp32 run's residue, in units of 2^-24 * sum |gy|
+    from pinned import U32, ZERO_BIAS_K, ZERO_GRAD_BIAS
+    assert sorted(absum) == sorted(ZERO_GRAD_BIAS)
+    res = max(float((np.abs(g32[n]) / (U32 * absum[n])).max()) for n in ZERO_GRAD_BIAS)
+    print(f"\n[{name}] float32 oracle zero-bias residue {res:.2f} x 2^-24 sum|gy|")
+    assert res <= ZERO_BIAS_K
+
+
+def test_reference_zero_bias_noise_record():
+    """tests/golden/bias_noise_b256.npz (make_bias_noise.py: the reference run here at B=256 in
+    float64 and float32): the 19 analytically-zero conv biases, and the reference's own fp32
+    residue on them in units of 2^-24 * sum |gy| -- the scale of the GPU gate (tests/pinned.py)."""
+    from pinned import U32, ZERO_BIAS_K, ZERO_GRAD_BIAS
+    z = np.load(os.path.join(GOLDEN, "bias_noise_b256.npz"))
+    assert int(z["batch"]) == 256
+    assert sorted(n + ".bias" for n in z["names"]) == sorted(ZERO_GRAD_BIAS)
+    ratios = [float((np.abs(z["db32/" + n]) / (U32 * z["absum/" + n])).max()) for n in z["names"]]
+    f64 = [float((np.abs(z["db64/" + n]) / (U32 * z["absum/" + n])).max()) for n in z["names"]]
+    print(f"\nreference fp32 residue at B=256: max {max(ratios):.3f} x 2^-24 sum|gy|; fp64 {max(f64):.1e}")
+    assert max(ratios) < 1.0 and max(f64) < 1e-6 and ZERO_BIAS_K >= 1.0

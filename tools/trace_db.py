@@ -13,7 +13,8 @@ def family(name: str) -> str:
     n = name.split("(")[0]
     for key, fam in (("conv3x3_pipe_kernel", "conv"), ("conv_first_fwd", "conv_first"),
                      ("wgrad_pipe", "wgrad"), ("wgrad_split", "wgrad"), ("wgrad_reduce", "wgrad_reduce"),
-                     ("in_bwd_edge_kernel<1", "edge_first"), ("in_bwd_edge_kernel<3", "edge_final"),
+                     ("in_bwd_edge_kernelILi1", "edge_final"), ("in_bwd_edge_kernelILi2", "edge_first"),
+                     ("in_bwd_edge_kernelILi3", "edge_first"),
                      ("in_bwd_kernel", "in_bwd_apply"), ("net_end", "net_end"), ("heads", "heads"),
                      ("adam", "adam"), ("pack", "pack"), ("loss", "loss")):
         if key in n:
