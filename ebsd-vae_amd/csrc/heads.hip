@@ -5,155 +5,177 @@
 //   std    = exp(logvar / 2) ;  z = mu + eps * std                (Normal(mu,std).rsample)
 //   dec_in = (z @ W2^T + b2).view(B, C, S, S)   -> written NHWC for the decoder
 //
-// One 1024-thread workgroup per pattern (16 waves: the heads sit on the critical path
-// between encoder and decoder, so latency matters more than the tiny FLOP count): the
-// F-wide feature row lives in LDS, each thread dots its k-slice against every head row
-// (coalesced weight rows), and the per-output sums fold through wave shuffles + LDS in a
-// fixed order.  The NCHW<->NHWC flatten permutation is folded into the LDS index, so the
-// NHWC encoder output never needs a transpose pass.
+// Three small launches per direction, each spread over >= 256 blocks so that every weight and
+// activation byte is read once from HBM (the heads are a few MFLOP: what costs is bandwidth
+// and latency, and a block-per-pattern layout re-reads every weight matrix B times):
+//   heads_dot_partial   split-K over the S*S feature pixels: block (pixel hw, pattern tile)
+//                       dots its patterns' C features at hw (contiguous in the NHWC input) with
+//                       the C matching weight columns (k = c*S*S + hw) of every output row,
+//                       staged in LDS; partial sums per (pixel, pattern, output) go to `work`
+//                       and the NCHW copy of the inputs (flat / g_out) is written on the way
+//   heads_*_finalize    per (pattern, latent): the S*S partials summed in pixel order, then
+//                       bias + reparameterisation (forward) or the reparameterisation adjoint
+//   heads_expand        per (pixel hw, pattern tile): the rank-L (2L) product back to the F
+//                       features of pixel hw, written NHWC (linear2 / g_enc), coalesced over c
+// Every sum has a fixed order: results are deterministic run to run.
 #include "common.h"
 #include "../../include/ebsdvae.h"
 
 namespace ev {
 
 constexpr int MAXL = 64;
-constexpr int HT = 1024;         // threads per pattern
-constexpr int HW_ = HT / 64;     // waves per pattern
-constexpr int OCH = 32;          // head outputs per register chunk
+constexpr int HT = 256;          // threads per heads block
 
-// MU_ONLY: the encoder-only inference path (DiffractionPatternIndexer.build_dictionary
-// consumes mu alone, latice/index/dp_indexer.py:136): only the mu head is evaluated.
-template <bool MU_ONLY>
-__global__ __launch_bounds__(HT) void heads_fwd_kernel(
-    const float* __restrict__ enc, const float* __restrict__ wmu, const float* __restrict__ bmu,
-    const float* __restrict__ wlv, const float* __restrict__ blv, const float* __restrict__ w2,
-    const float* __restrict__ b2, const float* __restrict__ eps, float* __restrict__ flat,
-    float* __restrict__ mu, float* __restrict__ stdo, float* __restrict__ z,
-    float* __restrict__ dec, int C, int S, int L) {
+// output rows padded to a power of two in 16..128 (2L <= 128)
+static int heads_np(int n) {
+  int p = 16;
+  while (p < n) p *= 2;
+  return p;
+}
+
+// Partial dots of one feature pixel: part[(hw * B + b) * NP + n] = sum_c A[b, hw, c] * Wrow_n[c*SS + hw]
+// MODE 0: rows = [Wmu; Wlv] (N = 2L) or Wmu (N = L), Wrow_n[k] = w[n * F + k];
+// MODE 1: rows = W2^T (N = L), Wrow_n[k] = W2[k * L + n].
+// R = BT * NP / 256 patterns per thread; copy (if given) receives A in NCHW flatten order at
+// copy[b * cstride + coff + k].
+template <int MODE, int R>
+__global__ __launch_bounds__(HT) void heads_dot_partial_kernel(
+    const float* __restrict__ A, const float* __restrict__ w0, const float* __restrict__ w1,
+    float* __restrict__ part, float* __restrict__ copy, int cstride, int coff, int B, int C,
+    int SS, int L, int N, int NP, int BT) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int F = C * S * S;
-  float* f = sm;                  // [F]
-  float* red = sm + F;            // [HW_][2 * MAXL]
-  float* zs = red + HW_ * 2 * MAXL;   // [MAXL]
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* e = enc + (size_t)b * F;
-  for (int i = tid; i < F; i += HT) {   // i = NHWC index within the pattern
-    const int c = i % C, hw = i / C;
-    f[c * S * S + hw] = e[i];
+  float* Wl = sm;                  // [C][NP]
+  float* Al = sm + C * NP;         // [BT][C + 1]
+  const int hw = blockIdx.x, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x;
+  const int F = C * SS;
+  for (int i = tid; i < C * NP; i += HT) {
+    const int k = i / NP, n = i - k * NP;
+    const int kk = k * SS + hw;
+    float v = 0.f;
+    if (MODE == 0) {
+      if (n < L) v = w0[(size_t)n * F + kk];
+      else if (n < N) v = w1[(size_t)(n - L) * F + kk];
+    } else {
+      if (n < N) v = w0[(size_t)kk * L + n];
+    }
+    Wl[i] = v;
+  }
+  for (int i = tid; i < BT * C; i += HT) {
+    const int bl = i / C, c = i - bl * C;
+    const int b = b0 + bl;
+    float v = 0.f;
+    if (b < B) {
+      v = A[((size_t)b * SS + hw) * C + c];
+      if (copy) copy[(size_t)b * cstride + coff + c * SS + hw] = v;
+    }
+    Al[bl * (C + 1) + c] = v;
   }
   __syncthreads();
-  if (!MU_ONLY)
-    for (int k = tid; k < F; k += HT) flat[(size_t)b * F + k] = f[k];
-  const int NO = MU_ONLY ? L : 2 * L;
-  for (int o0 = 0; o0 < NO; o0 += OCH) {
-    float acc[OCH];
+  const int n = tid % NP, bq = tid / NP, PB = HT / NP;
+  float acc[R];
 #pragma unroll
-    for (int j = 0; j < OCH; ++j) acc[j] = 0.f;
-    for (int k = tid; k < F; k += HT) {
-      const float fk = f[k];
+  for (int i = 0; i < R; ++i) acc[i] = 0.f;
+  for (int k = 0; k < C; ++k) {
+    const float w = Wl[k * NP + n];
 #pragma unroll
-      for (int j = 0; j < OCH; ++j) {
-        const int o = o0 + j;
-        if (o < NO) acc[j] = fmaf(fk, (o < L) ? wmu[(size_t)o * F + k] : wlv[(size_t)(o - L) * F + k], acc[j]);
-      }
-    }
+    for (int i = 0; i < R; ++i) acc[i] = fmaf(Al[(bq + i * PB) * (C + 1) + k], w, acc[i]);
+  }
 #pragma unroll
-    for (int j = 0; j < OCH; ++j) {
-      const float v = wave_sum(acc[j]);
-      if (lane == 0 && o0 + j < NO) red[wave * 2 * MAXL + o0 + j] = v;
-    }
-  }
-  __syncthreads();
-  if (MU_ONLY) {
-    if (tid < L) {
-      float m = bmu[tid];
-      for (int w = 0; w < HW_; ++w) m += red[w * 2 * MAXL + tid];
-      mu[(size_t)b * L + tid] = m;
-    }
-    return;
-  }
-  if (tid < L) {
-    float m = bmu[tid], lv = blv[tid];
-    for (int w = 0; w < HW_; ++w) {
-      m += red[w * 2 * MAXL + tid];
-      lv += red[w * 2 * MAXL + L + tid];
-    }
-    const float sd = expf(lv * 0.5f);
-    const float zz = fmaf(eps[(size_t)b * L + tid], sd, m);
-    mu[(size_t)b * L + tid] = m;
-    stdo[(size_t)b * L + tid] = sd;
-    z[(size_t)b * L + tid] = zz;
-    zs[tid] = zz;
-  }
-  __syncthreads();
-  for (int o = tid; o < F; o += HT) {
-    const float* wr = w2 + (size_t)o * L;
-    float s = b2[o];
-    for (int j = 0; j < L; ++j) s = fmaf(wr[j], zs[j], s);
-    const int c = o / (S * S), hw = o - c * (S * S);
-    dec[((size_t)b * S * S + hw) * C + c] = s;
+  for (int i = 0; i < R; ++i) {
+    const int b = b0 + bq + i * PB;
+    if (b < B && n < N) part[((size_t)hw * B + b) * NP + n] = acc[i];
   }
 }
 
-// gs layout per pattern: [g_mu_tot (L) | g_logvar (L) | g_out (F)]
-__global__ __launch_bounds__(HT) void heads_bwd_kernel(
-    const float* __restrict__ gdec, const float* __restrict__ gz, const float* __restrict__ gmu,
+// forward finalize: thread (b, j): mu, std, z (MU_ONLY: mu)
+template <bool MU_ONLY>
+__global__ __launch_bounds__(HT) void heads_fwd_finalize_kernel(
+    const float* __restrict__ part, const float* __restrict__ bmu, const float* __restrict__ blv,
+    const float* __restrict__ eps, float* __restrict__ mu, float* __restrict__ stdo,
+    float* __restrict__ z, int B, int SS, int L, int NP) {
+  const int i = blockIdx.x * HT + threadIdx.x;
+  if (i >= B * L) return;
+  const int b = i / L, j = i - b * L;
+  float m = 0.f, lv = 0.f;
+  for (int hw = 0; hw < SS; ++hw) {
+    const float* p = part + ((size_t)hw * B + b) * NP;
+    m += p[j];
+    if (!MU_ONLY) lv += p[L + j];
+  }
+  m += bmu[j];
+  mu[i] = m;
+  if (MU_ONLY) return;
+  lv += blv[j];
+  const float sd = expf(lv * 0.5f);
+  stdo[i] = sd;
+  z[i] = fmaf(eps[i], sd, m);
+}
+
+// backward finalize: thread (b, j): g_z total (linear2 adjoint + direct), then the
+// reparameterisation adjoint into gs = [g_mu_tot | g_logvar | g_out] (g_out: the partial pass)
+__global__ __launch_bounds__(HT) void heads_bwd_finalize_kernel(
+    const float* __restrict__ part, const float* __restrict__ gz, const float* __restrict__ gmu,
     const float* __restrict__ gstd, const float* __restrict__ stdv, const float* __restrict__ eps,
-    const float* __restrict__ wmu, const float* __restrict__ wlv, const float* __restrict__ w2,
-    float* __restrict__ genc, float* __restrict__ gs, int C, int S, int L) {
+    float* __restrict__ gs, int B, int SS, int L, int NP, int G) {
+  const int i = blockIdx.x * HT + threadIdx.x;
+  if (i >= B * L) return;
+  const int b = i / L, j = i - b * L;
+  float gzt = 0.f;
+  for (int hw = 0; hw < SS; ++hw) gzt += part[((size_t)hw * B + b) * NP + j];
+  if (gz) gzt += gz[i];
+  const float gmt = gzt + (gmu ? gmu[i] : 0.f);
+  const float glv = ((gstd ? gstd[i] : 0.f) + gzt * eps[i]) * stdv[i] * 0.5f;
+  gs[(size_t)b * G + j] = gmt;
+  gs[(size_t)b * G + L + j] = glv;
+}
+
+// out[b, hw, c] (NHWC) = bias[c*SS + hw] + sum_j V[b, j] * M[c*SS + hw][j]
+// MODE 0 (linear2): V = z (J = L, vstride L), M[k][j] = W2[k * L + j], bias b2
+// MODE 1 (g_enc):   V = gs[:, 0:2L] (J = 2L, vstride G), M[k][j] = j < L ? Wmu[j][k] : Wlv[j-L][k]
+template <int MODE, int R>
+__global__ __launch_bounds__(HT) void heads_expand_kernel(
+    const float* __restrict__ V, int vstride, const float* __restrict__ m0,
+    const float* __restrict__ m1, const float* __restrict__ bias, float* __restrict__ out, int B,
+    int C, int SS, int L, int J, int BT) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int F = C * S * S;
-  float* go = sm;                   // [F] g_out in flat (NCHW) order
-  float* red = sm + F;              // [HW_][MAXL]
-  float* gl = red + HW_ * MAXL;     // [2L]: g_mu_tot, g_logvar
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* gsb = gs + (size_t)b * (2 * L + F);
-  for (int i = tid; i < F; i += HT) {
-    const int c = i % C, hw = i / C;
-    go[c * S * S + hw] = gdec[(size_t)b * F + i];
-  }
-  __syncthreads();
-  for (int o = tid; o < F; o += HT) gsb[2 * L + o] = go[o];
-  for (int j0 = 0; j0 < L; j0 += 16) {   // g_z[j] = sum_o g_out[o] * W2[o][j]
-    float acc[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-    for (int o = tid; o < F; o += HT) {
-      const float g = go[o];
-      const float* wr = w2 + (size_t)o * L + j0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j0 + j < L) acc[j] = fmaf(g, wr[j], acc[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float v = wave_sum(acc[j]);
-      if (lane == 0 && j0 + j < L) red[wave * MAXL + j0 + j] = v;
+  float* Ml = sm;                  // [J][C]
+  float* Vl = sm + J * C;          // [BT][J]
+  const int hw = blockIdx.x, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x;
+  const int F = C * SS;
+  for (int i = tid; i < J * C; i += HT) {
+    float v;
+    if (MODE == 0) {
+      const int c = i / J, j = i - c * J;   // W2 rows: j fastest (contiguous)
+      v = m0[(size_t)(c * SS + hw) * L + j];
+      Ml[j * C + c] = v;
+    } else {
+      const int j = i / C, c = i - j * C;
+      v = j < L ? m0[(size_t)j * F + c * SS + hw] : m1[(size_t)(j - L) * F + c * SS + hw];
+      Ml[i] = v;
     }
   }
-  __syncthreads();
-  if (tid < L) {
-    const int j = tid;
-    const size_t bj = (size_t)b * L + j;
-    float gzt = gz ? gz[bj] : 0.f;
-    for (int w = 0; w < HW_; ++w) gzt += red[w * MAXL + j];
-    const float sd = stdv[bj];
-    const float gmt = gzt + (gmu ? gmu[bj] : 0.f);
-    const float glv = ((gstd ? gstd[bj] : 0.f) + gzt * eps[bj]) * sd * 0.5f;
-    gl[j] = gmt;
-    gl[L + j] = glv;
-    gsb[j] = gmt;
-    gsb[L + j] = glv;
+  for (int i = tid; i < BT * J; i += HT) {
+    const int bl = i / J, j = i - bl * J;
+    const int b = b0 + bl;
+    Vl[i] = b < B ? V[(size_t)b * vstride + j] : 0.f;
   }
   __syncthreads();
-  for (int k = tid; k < F; k += HT) {
-    float s = 0.f;
-    for (int j = 0; j < L; ++j) {
-      s = fmaf(gl[j], wmu[(size_t)j * F + k], s);
-      s = fmaf(gl[L + j], wlv[(size_t)j * F + k], s);
-    }
-    const int c = k / (S * S), hw = k - c * (S * S);
-    genc[((size_t)b * S * S + hw) * C + c] = s;
+  const int c = tid % C, bq = tid / C, PB = HT / C;
+  const float bb = MODE == 0 ? bias[c * SS + hw] : 0.f;
+  float acc[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) acc[i] = bb;
+  for (int j = 0; j < J; ++j) {
+    const float m = Ml[j * C + c];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = fmaf(Vl[(bq + i * PB) * J + j], m, acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int b = b0 + bq + i * PB;
+    if (b < B) out[((size_t)b * SS + hw) * C + c] = acc[i];
   }
 }
 
@@ -330,63 +352,129 @@ __global__ void normal_fill_kernel(float* __restrict__ out, int64_t n, uint64_t 
 
 using namespace ev;
 
+// ------------------------------------------------------------------ host side
+namespace {
+
+// pattern tile of a per-pixel launch with n lanes per pattern: R = BT * n / 256 in {1,2,4,8},
+// as few blocks as still gives >= 256 of them (SS pixels x ceil(B / BT) tiles)
+int heads_tile(int B, int SS, int n) {
+  int bt = 2048 / n;
+  while (bt > 256 / n && (long)SS * ((B + bt - 1) / bt) < 256) bt /= 2;
+  return bt;
+}
+
+template <typename K>
+void heads_lds_attr(K kernel, size_t lds) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+}
+
+template <int MODE>
+int launch_partial(const float* A, const float* w0, const float* w1, float* part, float* copy,
+                   int cstride, int coff, int B, int C, int SS, int L, int N, hipStream_t st) {
+  const int NP = heads_np(N);
+  const int bt = heads_tile(B, SS, NP);
+  const int R = bt * NP / HT;
+  const size_t lds = ((size_t)C * NP + (size_t)bt * (C + 1)) * sizeof(float);
+  EV_REQUIRE(lds <= 160 * 1024, "heads: feature channels %d too many", C);
+  const dim3 grid(SS, (B + bt - 1) / bt);
+#define EV_HP(RR)                                                                              \
+  case RR:                                                                                     \
+    heads_lds_attr(heads_dot_partial_kernel<MODE, RR>, lds);                                   \
+    hipLaunchKernelGGL((heads_dot_partial_kernel<MODE, RR>), grid, dim3(HT), lds, st, A, w0, w1, \
+                       part, copy, cstride, coff, B, C, SS, L, N, NP, bt);                     \
+    break;
+  switch (R) {
+    EV_HP(1) EV_HP(2) EV_HP(4) EV_HP(8)
+    default: EV_REQUIRE(false, "heads: tile %d x %d", bt, NP);
+  }
+#undef EV_HP
+  return 0;
+}
+
+template <int MODE>
+int launch_expand(const float* V, int vstride, const float* m0, const float* m1, const float* bias,
+                  float* out, int B, int C, int SS, int L, int J, hipStream_t st) {
+  const int bt = heads_tile(B, SS, C);
+  const int R = bt * C / HT;
+  const size_t lds = ((size_t)J * C + (size_t)bt * J) * sizeof(float);
+  EV_REQUIRE(lds <= 160 * 1024, "heads: expand tile too large");
+  const dim3 grid(SS, (B + bt - 1) / bt);
+#define EV_HE(RR)                                                                              \
+  case RR:                                                                                     \
+    heads_lds_attr(heads_expand_kernel<MODE, RR>, lds);                                        \
+    hipLaunchKernelGGL((heads_expand_kernel<MODE, RR>), grid, dim3(HT), lds, st, V, vstride, m0, \
+                       m1, bias, out, B, C, SS, L, J, bt);                                     \
+    break;
+  switch (R) {
+    EV_HE(1) EV_HE(2) EV_HE(4) EV_HE(8)
+    default: EV_REQUIRE(false, "heads: expand tile %d x %d", bt, C);
+  }
+#undef EV_HE
+  return 0;
+}
+
+bool heads_shape_ok(int B, int C, int S, int L) {
+  return B > 0 && L > 0 && L <= MAXL && S > 0 && S <= 1024 && C >= 16 && C <= 256 &&
+         (C & (C - 1)) == 0;
+}
+
+}  // namespace
+
+extern "C" size_t ebsdvae_heads_work(int B, int C, int S, int L) {
+  if (!heads_shape_ok(B, C, S, L)) return 0;
+  return (size_t)S * S * B * heads_np(2 * L) * sizeof(float);
+}
+
 extern "C" int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const float* b_mu,
                                  const float* w_lv, const float* b_lv, const float* w_l2,
                                  const float* b_l2, const float* eps, float* flat, float* mu,
-                                 float* std, float* z, float* dec_in, int B, int C, int S, int L,
-                                 ebsdvae_stream_t stream) {
+                                 float* std, float* z, float* dec_in, void* work, int B, int C,
+                                 int S, int L, ebsdvae_stream_t stream) {
   EV_REQUIRE(enc && w_mu && b_mu && w_lv && b_lv && w_l2 && b_l2 && eps && flat && mu && std && z &&
-                 dec_in,
+                 dec_in && work,
              "heads_fwd: null pointer");
-  EV_REQUIRE(B > 0 && L > 0 && L <= MAXL && C > 0 && S > 0, "heads_fwd: bad shape L=%d", L);
-  const int F = C * S * S;
-  const size_t lds = (F + (HW_ * 2 + 1) * MAXL) * sizeof(float);
-  EV_REQUIRE(lds <= 160 * 1024, "heads_fwd: feature width %d too large", F);
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute((const void*)heads_fwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    once = true;
-  }
-  hipLaunchKernelGGL(heads_fwd_kernel<false>, dim3(B), dim3(HT), lds, (hipStream_t)stream, enc, w_mu, b_mu,
-                     w_lv, b_lv, w_l2, b_l2, eps, flat, mu, std, z, dec_in, C, S, L);
+  EV_REQUIRE(heads_shape_ok(B, C, S, L), "heads_fwd: bad shape B=%d C=%d S=%d L=%d", B, C, S, L);
+  hipStream_t st = (hipStream_t)stream;
+  const int SS = S * S, F = C * SS;
+  float* part = (float*)work;
+  if (launch_partial<0>(enc, w_mu, w_lv, part, flat, F, 0, B, C, SS, L, 2 * L, st)) return 1;
+  hipLaunchKernelGGL(heads_fwd_finalize_kernel<false>, dim3((B * L + HT - 1) / HT), dim3(HT), 0, st,
+                     part, b_mu, b_lv, eps, mu, std, z, B, SS, L, heads_np(2 * L));
+  if (launch_expand<0>(z, L, w_l2, nullptr, b_l2, dec_in, B, C, SS, L, L, st)) return 1;
   return evh::check_launch("heads_fwd");
 }
 
 extern "C" int ebsdvae_latent_mu(const float* enc, const float* w_mu, const float* b_mu, float* mu,
-                                 int B, int C, int S, int L, ebsdvae_stream_t stream) {
-  EV_REQUIRE(enc && w_mu && b_mu && mu, "latent_mu: null pointer");
-  EV_REQUIRE(B > 0 && L > 0 && L <= MAXL && C > 0 && S > 0, "latent_mu: bad shape L=%d", L);
-  const int F = C * S * S;
-  const size_t lds = (F + (HW_ * 2 + 1) * MAXL) * sizeof(float);
-  EV_REQUIRE(lds <= 160 * 1024, "latent_mu: feature width %d too large", F);
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute((const void*)heads_fwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    once = true;
-  }
-  hipLaunchKernelGGL(heads_fwd_kernel<true>, dim3(B), dim3(HT), lds, (hipStream_t)stream, enc, w_mu,
-                     b_mu, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, mu, nullptr, nullptr,
-                     nullptr, C, S, L);
+                                 void* work, int B, int C, int S, int L, ebsdvae_stream_t stream) {
+  EV_REQUIRE(enc && w_mu && b_mu && mu && work, "latent_mu: null pointer");
+  EV_REQUIRE(heads_shape_ok(B, C, S, L), "latent_mu: bad shape B=%d C=%d S=%d L=%d", B, C, S, L);
+  hipStream_t st = (hipStream_t)stream;
+  const int SS = S * S;
+  float* part = (float*)work;
+  if (launch_partial<0>(enc, w_mu, nullptr, part, nullptr, 0, 0, B, C, SS, L, L, st)) return 1;
+  hipLaunchKernelGGL(heads_fwd_finalize_kernel<true>, dim3((B * L + HT - 1) / HT), dim3(HT), 0, st,
+                     part, b_mu, nullptr, nullptr, mu, nullptr, nullptr, B, SS, L, heads_np(L));
   return evh::check_launch("latent_mu");
 }
 
 extern "C" int ebsdvae_heads_bwd(const float* g_dec, const float* g_z, const float* g_mu,
                                  const float* g_std, const float* std, const float* eps,
                                  const float* w_mu, const float* w_lv, const float* w_l2,
-                                 float* g_enc, float* gs, int B, int C, int S, int L,
+                                 float* g_enc, float* gs, void* work, int B, int C, int S, int L,
                                  ebsdvae_stream_t stream) {
-  EV_REQUIRE(g_dec && std && eps && w_mu && w_lv && w_l2 && g_enc && gs, "heads_bwd: null pointer");
-  EV_REQUIRE(B > 0 && L > 0 && L <= MAXL, "heads_bwd: bad shape");
-  const int F = C * S * S;
-  const size_t lds = (F + (HW_ + 2) * MAXL) * sizeof(float);
-  EV_REQUIRE(lds <= 160 * 1024, "heads_bwd: feature width too large");
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute((const void*)heads_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    once = true;
-  }
-  hipLaunchKernelGGL(heads_bwd_kernel, dim3(B), dim3(HT), lds, (hipStream_t)stream, g_dec, g_z, g_mu,
-                     g_std, std, eps, w_mu, w_lv, w_l2, g_enc, gs, C, S, L);
+  EV_REQUIRE(g_dec && std && eps && w_mu && w_lv && w_l2 && g_enc && gs && work,
+             "heads_bwd: null pointer");
+  EV_REQUIRE(heads_shape_ok(B, C, S, L), "heads_bwd: bad shape B=%d C=%d S=%d L=%d", B, C, S, L);
+  hipStream_t st = (hipStream_t)stream;
+  const int SS = S * S, F = C * SS, G = 2 * L + F;
+  float* part = (float*)work;
+  // g_z partials (linear2 adjoint); g_out copied into gs in NCHW order for heads_wgrad
+  if (launch_partial<1>(g_dec, w_l2, nullptr, part, gs, G, 2 * L, B, C, SS, L, L, st)) return 1;
+  hipLaunchKernelGGL(heads_bwd_finalize_kernel, dim3((B * L + HT - 1) / HT), dim3(HT), 0, st, part,
+                     g_z, g_mu, g_std, std, eps, gs, B, SS, L, heads_np(L), G);
+  if (launch_expand<1>(gs, G, w_mu, w_lv, nullptr, g_enc, B, C, SS, L, 2 * L, st)) return 1;
   return evh::check_launch("heads_bwd");
 }
 

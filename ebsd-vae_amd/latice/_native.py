@@ -75,9 +75,10 @@ SIGNATURES = {
     "ebsdvae_in_bwd_final_tiles": [I, I],
     "ebsdvae_in_bwd_final_apply_max": [P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, P],
-    "ebsdvae_heads_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
-    "ebsdvae_heads_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
-    "ebsdvae_latent_mu": [P, P, P, P, I, I, I, I, P],
+    "ebsdvae_heads_work": [I, I, I, I],
+    "ebsdvae_heads_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_heads_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_latent_mu": [P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_heads_wgrad_work": [I, I, I],
     "ebsdvae_heads_wgrad": [P, P, P, P, P, P, P, P, P, P, I, I, I, P],
     "ebsdvae_linear_fwd": [P, P, P, P, I, I, I, P],
@@ -100,11 +101,11 @@ SIGNATURES = {
 _RESTYPE = {"ebsdvae_last_error": ctypes.c_char_p, "ebsdvae_wgrad_reduce_work": ctypes.c_size_t,
             "ebsdvae_wgrad_reduce_batch_work": ctypes.c_size_t,
             "ebsdvae_cosine_topk_work": ctypes.c_size_t,
-            "ebsdvae_heads_wgrad_work": ctypes.c_size_t, "ebsdvae_pack_split_bytes": ctypes.c_size_t}
+            "ebsdvae_heads_wgrad_work": ctypes.c_size_t, "ebsdvae_heads_work": ctypes.c_size_t, "ebsdvae_pack_split_bytes": ctypes.c_size_t}
 # queries that return a value rather than a status
 QUERIES = {"ebsdvae_version", "ebsdvae_conv_first_stat_tiles", "ebsdvae_conv3x3_stat_tiles", "ebsdvae_conv3x3_wgrad_slices",
            "ebsdvae_wgrad_reduce_batch_work", "ebsdvae_cosine_topk_work",
-           "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_in_bwd_final_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work",
+           "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_in_bwd_final_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work", "ebsdvae_heads_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
            "ebsdvae_conv3x3_split_pool_ok",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices", "ebsdvae_net_end_tiles"}

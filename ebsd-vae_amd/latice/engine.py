@@ -1115,14 +1115,25 @@ def encode_latents(plan: Plan, x, params, packs=None):
     enc, _ = encoder_forward(plan, x, params, packs=packs, train=False)
     B = x.shape[0]
     mu = _empty(B, plan.latent_dim, like=x)
+    work = _heads_work(B, plan, x)
     N.call("ebsdvae_latent_mu", N.ptr(enc), N.ptr(params["mu.0.weight"]), N.ptr(params["mu.0.bias"]),
-           N.ptr(mu), B, plan.enc_channels, plan.enc_side, plan.latent_dim, N.stream())
+           N.ptr(mu), N.ptr(work), B, plan.enc_channels, plan.enc_side, plan.latent_dim, N.stream())
     return mu
 
 
 # ----------------------------------------------------------------------------- heads
 HEAD_NAMES = ("mu.0.weight", "mu.0.bias", "logvar.0.weight", "logvar.0.bias",
               "linear2.0.weight", "linear2.0.bias")
+
+
+def _heads_work(B, plan: Plan, like):
+    """Split-K scratch of the heads launches (ebsdvae_heads_work bytes; stream-ordered reuse
+    through torch's caching allocator)."""
+    nbytes = N.call("ebsdvae_heads_work", B, plan.enc_channels, plan.enc_side, plan.latent_dim)
+    if nbytes <= 0:
+        raise RuntimeError(f"heads: unsupported shape C={plan.enc_channels} S={plan.enc_side} "
+                           f"L={plan.latent_dim}")
+    return torch.empty(nbytes // 4, dtype=torch.float32, device=like.device)
 
 
 def heads_forward(plan: Plan, enc, params, eps):
@@ -1134,8 +1145,10 @@ def heads_forward(plan: Plan, enc, params, eps):
     std = _empty(B, L, like=enc)
     z = _empty(B, L, like=enc)
     dec_in = _empty(B, s, s, C, like=enc)
+    work = _heads_work(B, plan, enc)
     N.call("ebsdvae_heads_fwd", N.ptr(enc), *[N.ptr(params[n]) for n in HEAD_NAMES], N.ptr(eps),
-           N.ptr(flat), N.ptr(mu), N.ptr(std), N.ptr(z), N.ptr(dec_in), B, C, s, L, N.stream())
+           N.ptr(flat), N.ptr(mu), N.ptr(std), N.ptr(z), N.ptr(dec_in), N.ptr(work), B, C, s, L,
+           N.stream())
     return flat, mu, std, z, dec_in
 
 
@@ -1147,7 +1160,8 @@ def heads_backward(plan: Plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, param
     gs = _empty(B, 2 * L + F, like=g_dec)
     N.call("ebsdvae_heads_bwd", N.ptr(g_dec), N.ptr(g_z), N.ptr(g_mu), N.ptr(g_std), N.ptr(std),
            N.ptr(eps), N.ptr(params["mu.0.weight"]), N.ptr(params["logvar.0.weight"]),
-           N.ptr(params["linear2.0.weight"]), N.ptr(g_enc), N.ptr(gs), B, C, s, L, N.stream())
+           N.ptr(params["linear2.0.weight"]), N.ptr(g_enc), N.ptr(gs), N.ptr(_heads_work(B, plan, g_dec)),
+           B, C, s, L, N.stream())
     out = {n: _grad_buf(grads, n, params[n]) for n in HEAD_NAMES}
     # the heads' weight gradients are off the critical path (g_enc is all the encoder
     # backward needs): on the side stream inside deferred_side_join() (the trainer's step)

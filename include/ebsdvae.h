@@ -336,22 +336,27 @@ int ebsdvae_upsample2_bwd(const float* g, float* out, int B, int H, int W, int C
  * enc: encoder output (B,S,S,C) NHWC.  flat = enc in NCHW flatten order (saved for
  * backward); mu/logvar = Linear(F,L); std = exp(logvar/2); z = mu + eps*std;
  * dec_in = Linear(L,F)(z) viewed (B,C,S,S) and written NHWC. */
+/* work: ebsdvae_heads_work(B,C,S,L) bytes of caller-owned device scratch (split-K partial
+ * sums over the S*S feature pixels; shared by heads_fwd / latent_mu / heads_bwd on one
+ * stream).  C: a power of two in 16..256; L <= 64. */
+size_t ebsdvae_heads_work(int B, int C, int S, int L);
 int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const float* b_mu,
                       const float* w_lv, const float* b_lv, const float* w_l2,
                       const float* b_l2, const float* eps, float* flat, float* mu,
-                      float* std, float* z, float* dec_in, int B, int C, int S, int L,
-                      ebsdvae_stream_t stream);
+                      float* std, float* z, float* dec_in, void* work, int B, int C, int S,
+                      int L, ebsdvae_stream_t stream);
 /* Encoder-only inference head: mu = Linear(F,L)(flatten_NCHW(enc)) (latice/model.py:55-58;
  * DiffractionPatternIndexer.build_dictionary consumes mu alone). */
-int ebsdvae_latent_mu(const float* enc, const float* w_mu, const float* b_mu, float* mu, int B,
-                      int C, int S, int L, ebsdvae_stream_t stream);
+int ebsdvae_latent_mu(const float* enc, const float* w_mu, const float* b_mu, float* mu,
+                      void* work, int B, int C, int S, int L, ebsdvae_stream_t stream);
 /* g_dec: grad of dec_in (B,S,S,C NHWC); g_z/g_mu/g_std: direct output grads (may be
  * NULL = 0).  Writes g_enc (B,S,S,C NHWC) and per-sample scratch
  * gs = [g_mu_tot (B,L) | g_logvar (B,L) | g_out (B,F)] consumed by heads_wgrad. */
 int ebsdvae_heads_bwd(const float* g_dec, const float* g_z, const float* g_mu,
                       const float* g_std, const float* std, const float* eps,
                       const float* w_mu, const float* w_lv, const float* w_l2, float* g_enc,
-                      float* gs, int B, int C, int S, int L, ebsdvae_stream_t stream);
+                      float* gs, void* work, int B, int C, int S, int L,
+                      ebsdvae_stream_t stream);
 /* Weight/bias gradients of the three Linear heads (autograd's addmm backward for
  * latice/model.py:127-131): deterministic split-batch reduction through `work`
  * (ebsdvae_heads_wgrad_work(B,F,L) bytes, caller-owned). */

@@ -94,8 +94,13 @@ int main() {
   expect_err(ebsdvae_conv3x3_cout1_fwd(nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0, 2, 128,
                                        128, 32, nullptr), "cout1 null");
   expect_err(ebsdvae_heads_fwd(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 128, 4, 16,
-                               nullptr), "heads_fwd null");
+                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 128,
+                               4, 16, nullptr), "heads_fwd null");
+  if (ebsdvae_heads_work(256, 128, 4, 16) != (size_t)16 * 256 * 32 * 4 ||
+      ebsdvae_heads_work(2, 96, 4, 16) != 0 || ebsdvae_heads_work(2, 128, 4, 65) != 0) {
+    printf("FAIL heads_work\n");
+    ++g_fail;
+  }
   expect_err(ebsdvae_in_bwd_reduce(nullptr, 0, nullptr, nullptr, nullptr, 2, 128, 128, 32, nullptr),
              "in_bwd_reduce null");
   expect_err(ebsdvae_in_bwd_apply_max(nullptr, 9, nullptr, nullptr, nullptr, nullptr, nullptr, 2,

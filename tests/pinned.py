@@ -35,7 +35,11 @@ ZERO_GRAD_BIAS = tuple(f"encoder.{i}.0.bias" for i in O.ENC_IDX) + tuple(
     f"decoder.{i}.0.bias" for i in O.DEC_IDX)
 DECISION_GATE = 1e-3
 STATE_GATE = 1e-4
-ZERO_BIAS_K = 4096.0     # residue <= 2.4e-4 of sum |gy| (units of 2^-24 * A_c)
+# residue gate, in units of 2^-24 * A_c (<= 6.1e-5 of sum |gy|).  Measured on MI355X (round 4,
+# every fixture, B = 4..256, all arithmetics and switches): f16x3 <= 3.0, bf16x6 <= 1.7, fp32
+# <= 181 (decoder.13.0 on vae128_b8_c1: the fp32 weight-gradient kernel's longer sequential
+# slice sums); the reference's own fp32 run at B = 256: 0.18 (bias_noise_b256.npz)
+ZERO_BIAS_K = 1024.0
 U32 = 2.0 ** -24
 
 

@@ -74,7 +74,7 @@ def test_invalid_shapes_report_errors_without_gpu():
     with pytest.raises(RuntimeError, match="cin=3"):
         _native.call("ebsdvae_conv3x3_fwd", 1, None, 0, 1, None, 1, None, None, 2, 16, 16, 3, 32, None)
     with pytest.raises(RuntimeError, match="null pointer"):
-        _native.call("ebsdvae_heads_fwd", *([None] * 13), 2, 128, 4, 16, None)
+        _native.call("ebsdvae_heads_fwd", *([None] * 14), 2, 128, 4, 16, None)
 
 
 def test_host_asan_driver():

@@ -26,12 +26,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--marker", default="adam_kernel",
+                    help="kernel that ends one iteration (c4 encoder-only batches: heads_fwd)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select d.start, d.end, s.kernel_name, d.stream_id, d.queue_id, s.arch_vgpr_count, "
                      "s.sgpr_count, s.private_segment_size from rocpd_kernel_dispatch d join "
                      "rocpd_info_kernel_symbol s on d.kernel_id = s.id order by d.start").fetchall()
-    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r[2]]
+    adam = [i for i, r in enumerate(rows) if a.marker in r[2]]
     i0, i1 = adam[-a.steps - 1], adam[-1]
     sel = rows[i0 + 1:i1 + 1]
     t0, t1 = rows[i0][1], rows[i1][1]
@@ -62,7 +65,7 @@ def main():
         d[1] += (e - s) / 1e3
         d[2] = (vg, sg, ps)
     print("\nkernels (us per launch, launches/step, vgpr/sgpr/scratch):")
-    for n, (k, us, res) in sorted(big.items(), key=lambda kv: -kv[1][1])[:40]:
+    for n, (k, us, res) in sorted(big.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"  {us / a.steps:8.1f} us/step {k // a.steps:3d}x {us / k:7.1f} us  {res}  {n[:110]}")
 
 
