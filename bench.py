@@ -479,8 +479,14 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rank_ms = None
     if world > 1:
+        # every rank's own time (the spread shows stragglers / RCCL waits), then the max
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tg = t if dist.get_backend() == "nccl" else t.cpu()
+        per = [torch.zeros_like(tg) for _ in range(world)]
+        dist.all_gather(per, tg)
+        rank_ms = [round(float(p) / args.steps * 1e3, 3) for p in per]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     loss = float(out[0])
@@ -547,6 +553,9 @@ def main():
                    "global_batch": world * args.batch, "image_size": args.image_size,
                    "latent_dim": args.latent_dim, "parallelism": f"dp{world}"},
         "process_group": pg,
+        "rank_ms_per_step": rank_ms,
+        "rank_spread_pct": (None if rank_ms is None else
+                            round(100.0 * (max(rank_ms) - min(rank_ms)) / max(rank_ms), 2)),
         "roofline": roof,
         "step_fp32_tflops": round(step_tflops, 2),
         "step_frac_of_fp32_peak": round(step_tflops / FP32_PEAK_TFLOPS, 4),

@@ -10,8 +10,8 @@
 // pass that writes the block's output gradient (ebsdvae_in_bwd_final_apply_max) reads g1 from
 // here and is unchanged.
 //
-// Block = one band of TH output rows of one image (W = 128: 8 channel groups x 32 pixel lanes,
-// 4 pixels per thread per row).  It streams the source rows r0-2 .. r0+TH+1 once: row q is
+// Block = one band of TH output rows of one image (W = 128 or 256: 8 channel groups x W/4 pixel
+// lanes, 4 pixels per thread per row; 256 or 512 threads).  It streams the source rows r0-2 .. r0+TH+1 once: row q is
 // normalised into a 4-row ring of a = lrelu(IN(y13)) in LDS; x_hat / g1 of row q-1 follow from
 // the ring (g1 into a 4-row ring); the reduce of row q-2 from the g1 ring and a.  Four slots
 // let every step write the slot of a row the previous step no longer reads, so two barriers
@@ -24,10 +24,15 @@
 
 namespace ev {
 
-constexpr int NE_C = 32, NE_W = 128, NE_TH = 16, NE_NTH = 256;
-constexpr int NE_WP = NE_W + 2;            // ring row: zero column, W pixels, zero column
-constexpr int NE_AROW = NE_WP * NE_C;      // floats per a-ring row
+constexpr int NE_C = 32, NE_TH = 16;
 constexpr int NE_RING = 4;                 // ring slots (a and g1): slot(row) = (row - r0 + k) & 3
+// per width: threads, ring row (zero column, W pixels, zero column), floats per a-ring row
+template <int W> constexpr int ne_nth() { return 2 * W; }
+template <int W> constexpr int ne_wp() { return W + 2; }
+template <int W> constexpr int ne_arow() { return (W + 2) * NE_C; }
+template <int W> constexpr size_t ne_lds() {
+  return (size_t)(NE_RING * ne_arow<W>() + NE_RING * ne_wp<W>()) * sizeof(float);
+}
 
 EV_DEVINL float ne_bce(float xh, float t) {
   return (1.f - t) * xh + fmaxf(-xh, 0.f) + log1pf(expf(-fabsf(xh)));
@@ -51,12 +56,14 @@ EV_DEVINL float ne_fold8(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
+template <int W>
+__global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
     const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
     const float* __restrict__ b14, const float* __restrict__ xt, const float* __restrict__ g_loss,
     float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
-  constexpr int C = NE_C, W = NE_W, TH = NE_TH, WP = NE_WP;
+  constexpr int C = NE_C, TH = NE_TH, WP = ne_wp<W>(), NE_AROW = ne_arow<W>();
+  constexpr int NE_NTH = ne_nth<W>(), NPL = W / 4, NWAVE = NE_NTH / 64;
   extern __shared__ __attribute__((aligned(16))) float ne_sm[];
   float* aring = ne_sm;                       // [4][WP][C]
   float* gring = ne_sm + NE_RING * NE_AROW;   // [4][WP]
@@ -86,13 +93,13 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
 
   const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + (size_t)b * HW * C), 0,
                                                     (int)(HW * C * 4), 0x00020000);
-  // row q of y13 for this thread: 4 pixels pl + 32 j, channels c .. c+3 (out-of-image rows
+  // row q of y13 for this thread: 4 pixels pl + NPL j, channels c .. c+3 (out-of-image rows
   // fall outside the buffer range and read 0; they are zeroed as conv padding anyway)
   auto load_row = [&](int q, float4 (&d)[4]) EV_LAMBDA_INLINE {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       d[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            ry, ((q * W + pl + 32 * j) * C + c) * 4, 0, 0));
+                                            ry, ((q * W + pl + NPL * j) * C + c) * 4, 0, 0));
   };
 
   double s1d[4] = {0.0, 0.0, 0.0, 0.0}, s2d[4] = {0.0, 0.0, 0.0, 0.0};
@@ -104,9 +111,9 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
   float bsum = 0.f, bce = 0.f;   // g1 and BCE sums over the band (lanes cg < 4)
 
   // the BCE target of x_hat row r0 - 3 + i, loaded two steps ahead: lanes cg < 4 own pixel
-  // pl + 32 cg of the row for the logit-gradient / BCE work (one evaluation per pixel)
+  // pl + NPL cg of the row for the logit-gradient / BCE work (one evaluation per pixel)
   auto load_tgt = [&](int r, float& d) EV_LAMBDA_INLINE {
-    d = (r >= 0 && r < H && cg < 4) ? xt[(size_t)b * HW + (size_t)r * W + pl + 32 * cg] : 0.f;
+    d = (r >= 0 && r < H && cg < 4) ? xt[(size_t)b * HW + (size_t)r * W + pl + NPL * cg] : 0.f;
   };
   float4 ybuf[2][4];
   float tbuf[2];
@@ -128,7 +135,7 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
         v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]), normact_fs(v.z, fs[2]),
                         normact_fs(v.w, fs[3]));
         if (!in) v = make_float4(0.f, 0.f, 0.f, 0.f);
-        st4(ar + (pl + 32 * j + 1) * C + c, v);
+        st4(ar + (pl + NPL * j + 1) * C + c, v);
       }
     }
     // prefetch row q + 2 into the registers just consumed
@@ -142,10 +149,10 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
       const float* a2 = aring + (i & 3) * NE_AROW;         // row q
       const bool inrow = r >= 0 && r < H, own = r >= r0 && r < r0 + TH;
       float* gr = gring + (i & 3) * WP;                    // g1 row r0 - 3 + i
-      float xsel = 0.f;   // x_hat of pixel pl + 32 cg (lanes cg < 4)
+      float xsel = 0.f;   // x_hat of pixel pl + NPL cg (lanes cg < 4)
 #pragma unroll 2
       for (int j = 0; j < 4; ++j) {
-        const int w = pl + 32 * j;
+        const int w = pl + NPL * j;
         pkf2 s = pk2(0.f, 0.f);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
@@ -158,7 +165,7 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
         xsel = cg == j ? xh : xsel;
       }
       if (cg < 4) {
-        const int w = pl + 32 * cg;
+        const int w = pl + NPL * cg;
         float g = 0.f;
         if (inrow) {
           g = cr * (ne_sigmoid(xsel) - tcur);
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
       float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int j = 0; j < 4; ++j) {
-        const int w = pl + 32 * j;
+        const int w = pl + NPL * j;
         // nb[t] = g1[p - d(t)]: tap (kh, kw) reads row (q-2) + 1 - kh, column w + 1 - kw
         float nb[9];
 #pragma unroll
@@ -231,10 +238,10 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
   }
   __syncthreads();
 
-  // ---- band partials, fixed order: lanes of a channel group in-wave, then the 4 waves
+  // ---- band partials, fixed order: lanes of a channel group in-wave, then the NWAVE waves
   const int lane = tid & 63, wave = tid >> 6;
   // (a tree of lane shuffles: a serial 32-step LDS walk here cost ~8 us per block)
-  double* red = reinterpret_cast<double*>(ne_sm);            // [4 waves][8 cg][8]
+  double* red = reinterpret_cast<double*>(ne_sm);            // [NWAVE][8 cg][8]
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     double v = k < 4 ? s1d[k] : s2d[k - 4];
@@ -249,12 +256,12 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
     const int g = tid >> 2, k = tid & 3;
     double u = 0.0, v = 0.0;
 #pragma unroll
-    for (int wv = 0; wv < 4; ++wv) { u += red[(wv * 8 + g) * 8 + k]; v += red[(wv * 8 + g) * 8 + 4 + k]; }
+    for (int wv = 0; wv < NWAVE; ++wv) { u += red[(wv * 8 + g) * 8 + k]; v += red[(wv * 8 + g) * 8 + 4 + k]; }
     part[(size_t)slice * C + tid] = make_double2(u, v);
   }
   __syncthreads();
   // weight-gradient partials [slice][tap][0][ci]: fold the 32 pixel lanes of each channel group
-  float* wred = ne_sm;   // [4 waves][8 cg][36 + 2]
+  float* wred = ne_sm;   // [NWAVE][8 cg][36 + 2]
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -274,13 +281,17 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
   __syncthreads();
   for (int i = tid; i < 8 * 36; i += NE_NTH) {
     const int g = i / 36, e = i % 36, k = e / 9, t = e % 9;
-    const float s = wred[(0 * 8 + g) * 38 + e] + wred[(1 * 8 + g) * 38 + e] +
-                    wred[(2 * 8 + g) * 38 + e] + wred[(3 * 8 + g) * 38 + e];
+    float s = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < NWAVE; ++wv) s += wred[(wv * 8 + g) * 38 + e];
     wpart[((size_t)slice * 9 + t) * 32 + g * 4 + k] = s;
   }
   if (tid == 0) {
-    bpart[slice] = wred[0 * 38 + 36] + wred[8 * 38 + 36] + wred[16 * 38 + 36] + wred[24 * 38 + 36];
-    bce_part[slice] = wred[0 * 38 + 37] + wred[8 * 38 + 37] + wred[16 * 38 + 37] + wred[24 * 38 + 37];
+    float bs = 0.f, es = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < NWAVE; ++wv) { bs += wred[wv * 8 * 38 + 36]; es += wred[wv * 8 * 38 + 37]; }
+    bpart[slice] = bs;
+    bce_part[slice] = es;
   }
 }
 
@@ -289,7 +300,23 @@ __global__ __launch_bounds__(NE_NTH, 2) void net_end_kernel(
 using namespace ev;
 
 extern "C" int ebsdvae_net_end_tiles(int H, int W) {
-  return (W == NE_W && ev_dim_ok(H) && H % NE_TH == 0) ? H / NE_TH : -1;
+  return ((W == 128 || W == 256) && ev_dim_ok(H) && H % NE_TH == 0) ? H / NE_TH : -1;
+}
+
+template <int W>
+static void net_end_launch(dim3 grid, hipStream_t st, const float* y13, const float* st13,
+                           const float* w14, const float* b14, const float* x, const float* g_loss,
+                           float gscale, float* x_hat, float* g1, float* bce_part, double* part,
+                           float* wpart, float* bpart, int H) {
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)net_end_kernel<W>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)ne_lds<W>());
+    once = true;
+  }
+  hipLaunchKernelGGL(net_end_kernel<W>, grid, dim3(ne_nth<W>()), ne_lds<W>(), st, y13,
+                     (const float2*)st13, w14, b14, x, g_loss, gscale, x_hat, g1, bce_part,
+                     (double2*)part, wpart, bpart, H);
 }
 
 extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float* w14, const float* b14,
@@ -299,18 +326,14 @@ extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float*
   EV_REQUIRE(y13 && st13 && w14 && x && x_hat && g1 && bce_part && part && wpart && bpart && B > 0,
              "net_end: null pointer");
   EV_REQUIRE(C == NE_C && ebsdvae_net_end_tiles(H, W) > 0,
-             "net_end: C=%d %dx%d unsupported (C 32, W %d, H a multiple of %d)", C, H, W, NE_W, NE_TH);
+             "net_end: C=%d %dx%d unsupported (C 32, W 128 or 256, H a multiple of %d)", C, H, W, NE_TH);
   const int T = H / NE_TH;
   const float gscale = scale / ((float)B * (float)(H * W));
-  const size_t lds = (size_t)(NE_RING * NE_AROW + NE_RING * NE_WP) * sizeof(float);
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute((const void*)net_end_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    once = true;
-  }
-  hipLaunchKernelGGL(net_end_kernel, dim3(T, B), dim3(NE_NTH), lds, (hipStream_t)stream, y13,
-                     (const float2*)st13, w14, b14, x, g_loss, gscale, x_hat, g1, bce_part,
-                     (double2*)part, wpart, bpart, H);
+  if (W == 128)
+    net_end_launch<128>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
+                        g1, bce_part, part, wpart, bpart, H);
+  else
+    net_end_launch<256>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
+                        g1, bce_part, part, wpart, bpart, H);
   return evh::check_launch("net_end");
 }

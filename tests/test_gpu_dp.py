@@ -123,4 +123,5 @@ def test_bench_self_launches_ranks(cuda):
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 16
     assert res["process_group"]["backend"] == "gloo" and res["process_group"]["world_size"] == 2
+    assert len(res["rank_ms_per_step"]) == 2 and res["rank_spread_pct"] >= 0
     assert "gloo grad all-reduce (rehearsal" in res["config"]["workload"]
