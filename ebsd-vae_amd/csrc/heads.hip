@@ -8,12 +8,13 @@
 // Three small launches per direction, each spread over >= 256 blocks so that every weight and
 // activation byte is read once from HBM (the heads are a few MFLOP: what costs is bandwidth
 // and latency, and a block-per-pattern layout re-reads every weight matrix B times):
-//   heads_dot_partial   split-K over the S*S feature pixels: block (pixel hw, pattern tile)
-//                       dots its patterns' C features at hw (contiguous in the NHWC input) with
-//                       the C matching weight columns (k = c*S*S + hw) of every output row,
-//                       staged in LDS; partial sums per (pixel, pattern, output) go to `work`
-//                       and the NCHW copy of the inputs (flat / g_out) is written on the way
-//   heads_*_finalize    per (pattern, latent): the S*S partials summed in pixel order, then
+//   heads_dot_partial   split-K over feature chunks of CC channels x S*S pixels (about 128
+//                       features, a contiguous range of the NCHW flatten, so every weight row is
+//                       read in one run): block (chunk, pattern tile) dots its patterns' chunk
+//                       with every output row's matching weights, both staged in LDS; partial
+//                       sums per (chunk, pattern, output) go to `work`, and the NCHW copy of the
+//                       inputs (flat / g_out) is written on the way
+//   heads_*_finalize    per (pattern, latent): the chunk partials summed in chunk order, then
 //                       bias + reparameterisation (forward) or the reparameterisation adjoint
 //   heads_expand        per (pixel hw, pattern tile): the rank-L (2L) product back to the F
 //                       features of pixel hw, written NHWC (linear2 / g_enc), coalesced over c
@@ -33,58 +34,67 @@ static int heads_np(int n) {
   return p;
 }
 
-// Partial dots of one feature pixel: part[(hw * B + b) * NP + n] = sum_c A[b, hw, c] * Wrow_n[c*SS + hw]
+// Partial dots over one chunk of the features: chunk g = CC consecutive channels c0 = g*CC ..
+// at every pixel, i.e. the contiguous feature range k = c0*SS .. (c0+CC)*SS - 1 of the NCHW
+// flatten (KC = CC*SS features; every weight row read in one contiguous run):
+//   part[(g * B + b) * NP + n] = sum_{k in chunk} A[b, k] * Wrow_n[k]
+// with A[b, k = c*SS + hw] = the NHWC input at (hw, c) (runs of CC channels).
 // MODE 0: rows = [Wmu; Wlv] (N = 2L) or Wmu (N = L), Wrow_n[k] = w[n * F + k];
 // MODE 1: rows = W2^T (N = L), Wrow_n[k] = W2[k * L + n].
 // R = BT * NP / 256 patterns per thread; copy (if given) receives A in NCHW flatten order at
-// copy[b * cstride + coff + k].
+// copy[b * cstride + coff + k] (contiguous runs of SS).
 template <int MODE, int R>
 __global__ __launch_bounds__(HT) void heads_dot_partial_kernel(
     const float* __restrict__ A, const float* __restrict__ w0, const float* __restrict__ w1,
     float* __restrict__ part, float* __restrict__ copy, int cstride, int coff, int B, int C,
-    int SS, int L, int N, int NP, int BT) {
+    int SS, int CC, int L, int N, int NP, int BT) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Wl = sm;                  // [C][NP]
-  float* Al = sm + C * NP;         // [BT][C + 1]
-  const int hw = blockIdx.x, b0 = blockIdx.y * BT;
+  const int KC = CC * SS, NPP = NP + 1;
+  float* Wl = sm;                  // [KC][NP + 1]
+  float* Al = sm + KC * NPP;       // [BT][KC + 1]
+  const int g = blockIdx.x, b0 = blockIdx.y * BT, c0 = g * CC;
   const int tid = threadIdx.x;
   const int F = C * SS;
-  for (int i = tid; i < C * NP; i += HT) {
-    const int k = i / NP, n = i - k * NP;
-    const int kk = k * SS + hw;
-    float v = 0.f;
-    if (MODE == 0) {
-      if (n < L) v = w0[(size_t)n * F + kk];
-      else if (n < N) v = w1[(size_t)(n - L) * F + kk];
-    } else {
-      if (n < N) v = w0[(size_t)kk * L + n];
+  const size_t k0 = (size_t)c0 * SS;
+  for (int i = tid; i < NP * KC; i += HT) {
+    if (MODE == 0) {   // row n, feature kk: contiguous in kk
+      const int n = i / KC, kk = i - n * KC;
+      float v = 0.f;
+      if (n < L) v = w0[(size_t)n * F + k0 + kk];
+      else if (n < N) v = w1[(size_t)(n - L) * F + k0 + kk];
+      Wl[kk * NPP + n] = v;
+    } else {           // W2 row k0 + kk, column n: contiguous in n
+      const int kk = i / NP, n = i - kk * NP;
+      Wl[kk * NPP + n] = n < N ? w0[(k0 + kk) * L + n] : 0.f;
     }
-    Wl[i] = v;
   }
-  for (int i = tid; i < BT * C; i += HT) {
-    const int bl = i / C, c = i - bl * C;
+  for (int i = tid; i < BT * KC; i += HT) {   // NHWC runs of CC channels
+    const int bl = i / KC, r = i - bl * KC;
+    const int hw = r / CC, ci = r - hw * CC;
     const int b = b0 + bl;
-    float v = 0.f;
-    if (b < B) {
-      v = A[((size_t)b * SS + hw) * C + c];
-      if (copy) copy[(size_t)b * cstride + coff + c * SS + hw] = v;
-    }
-    Al[bl * (C + 1) + c] = v;
+    Al[bl * (KC + 1) + ci * SS + hw] = b < B ? A[((size_t)b * SS + hw) * C + c0 + ci] : 0.f;
   }
   __syncthreads();
+  if (copy) {   // NCHW runs of SS pixels
+    for (int i = tid; i < BT * KC; i += HT) {
+      const int bl = i / KC, kk = i - bl * KC;
+      const int b = b0 + bl;
+      if (b < B) copy[(size_t)b * cstride + coff + k0 + kk] = Al[bl * (KC + 1) + kk];
+    }
+  }
   const int n = tid % NP, bq = tid / NP, PB = HT / NP;
   float acc[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) acc[i] = 0.f;
-  for (int k = 0; k < C; ++k) {
-    const float w = Wl[k * NP + n];
+  for (int k = 0; k < KC; ++k) {
+    const float w = Wl[k * NPP + n];
 #pragma unroll
-    for (int i = 0; i < R; ++i) acc[i] = fmaf(Al[(bq + i * PB) * (C + 1) + k], w, acc[i]);
+    for (int i = 0; i < R; ++i) acc[i] = fmaf(Al[(bq + i * PB) * (KC + 1) + k], w, acc[i]);
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int b = b0 + bq + i * PB;
-    if (b < B && n < N) part[((size_t)hw * B + b) * NP + n] = acc[i];
+    if (b < B && n < N) part[((size_t)g * B + b) * NP + n] = acc[i];
   }
 }
 
@@ -93,13 +103,13 @@ template <bool MU_ONLY>
 __global__ __launch_bounds__(HT) void heads_fwd_finalize_kernel(
     const float* __restrict__ part, const float* __restrict__ bmu, const float* __restrict__ blv,
     const float* __restrict__ eps, float* __restrict__ mu, float* __restrict__ stdo,
-    float* __restrict__ z, int B, int SS, int L, int NP) {
+    float* __restrict__ z, int B, int KS, int L, int NP) {
   const int i = blockIdx.x * HT + threadIdx.x;
   if (i >= B * L) return;
   const int b = i / L, j = i - b * L;
   float m = 0.f, lv = 0.f;
-  for (int hw = 0; hw < SS; ++hw) {
-    const float* p = part + ((size_t)hw * B + b) * NP;
+  for (int g = 0; g < KS; ++g) {   // the feature chunks in order
+    const float* p = part + ((size_t)g * B + b) * NP;
     m += p[j];
     if (!MU_ONLY) lv += p[L + j];
   }
@@ -117,12 +127,12 @@ __global__ __launch_bounds__(HT) void heads_fwd_finalize_kernel(
 __global__ __launch_bounds__(HT) void heads_bwd_finalize_kernel(
     const float* __restrict__ part, const float* __restrict__ gz, const float* __restrict__ gmu,
     const float* __restrict__ gstd, const float* __restrict__ stdv, const float* __restrict__ eps,
-    float* __restrict__ gs, int B, int SS, int L, int NP, int G) {
+    float* __restrict__ gs, int B, int KS, int L, int NP, int G) {
   const int i = blockIdx.x * HT + threadIdx.x;
   if (i >= B * L) return;
   const int b = i / L, j = i - b * L;
   float gzt = 0.f;
-  for (int hw = 0; hw < SS; ++hw) gzt += part[((size_t)hw * B + b) * NP + j];
+  for (int g = 0; g < KS; ++g) gzt += part[((size_t)g * B + b) * NP + j];
   if (gz) gzt += gz[i];
   const float gmt = gzt + (gmu ? gmu[i] : 0.f);
   const float glv = ((gstd ? gstd[i] : 0.f) + gzt * eps[i]) * stdv[i] * 0.5f;
@@ -370,20 +380,30 @@ void heads_lds_attr(K kernel, size_t lds) {
                               (int)lds);
 }
 
+// feature chunks of the partial pass: CC channels (a power of two dividing C) x all SS pixels,
+// about 128 features each; KS = C / CC chunks
+int heads_cc(int C, int SS) {
+  int cc = 1;
+  while (cc * 2 * SS <= 128 && cc * 2 <= C) cc *= 2;
+  return cc;
+}
+int heads_ks(int C, int SS) { return C / heads_cc(C, SS); }
+
 template <int MODE>
 int launch_partial(const float* A, const float* w0, const float* w1, float* part, float* copy,
                    int cstride, int coff, int B, int C, int SS, int L, int N, hipStream_t st) {
   const int NP = heads_np(N);
-  const int bt = heads_tile(B, SS, NP);
+  const int CC = heads_cc(C, SS), KS = C / CC, KC = CC * SS;
+  const int bt = heads_tile(B, KS, NP);
   const int R = bt * NP / HT;
-  const size_t lds = ((size_t)C * NP + (size_t)bt * (C + 1)) * sizeof(float);
-  EV_REQUIRE(lds <= 160 * 1024, "heads: feature channels %d too many", C);
-  const dim3 grid(SS, (B + bt - 1) / bt);
+  const size_t lds = ((size_t)KC * (NP + 1) + (size_t)bt * (KC + 1)) * sizeof(float);
+  EV_REQUIRE(lds <= 160 * 1024, "heads: feature chunk of %d too large", KC);
+  const dim3 grid(KS, (B + bt - 1) / bt);
 #define EV_HP(RR)                                                                              \
   case RR:                                                                                     \
     heads_lds_attr(heads_dot_partial_kernel<MODE, RR>, lds);                                   \
     hipLaunchKernelGGL((heads_dot_partial_kernel<MODE, RR>), grid, dim3(HT), lds, st, A, w0, w1, \
-                       part, copy, cstride, coff, B, C, SS, L, N, NP, bt);                     \
+                       part, copy, cstride, coff, B, C, SS, CC, L, N, NP, bt);                 \
     break;
   switch (R) {
     EV_HP(1) EV_HP(2) EV_HP(4) EV_HP(8)
@@ -424,7 +444,7 @@ bool heads_shape_ok(int B, int C, int S, int L) {
 
 extern "C" size_t ebsdvae_heads_work(int B, int C, int S, int L) {
   if (!heads_shape_ok(B, C, S, L)) return 0;
-  return (size_t)S * S * B * heads_np(2 * L) * sizeof(float);
+  return (size_t)heads_ks(C, S * S) * B * heads_np(2 * L) * sizeof(float);
 }
 
 extern "C" int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const float* b_mu,
@@ -441,7 +461,7 @@ extern "C" int ebsdvae_heads_fwd(const float* enc, const float* w_mu, const floa
   float* part = (float*)work;
   if (launch_partial<0>(enc, w_mu, w_lv, part, flat, F, 0, B, C, SS, L, 2 * L, st)) return 1;
   hipLaunchKernelGGL(heads_fwd_finalize_kernel<false>, dim3((B * L + HT - 1) / HT), dim3(HT), 0, st,
-                     part, b_mu, b_lv, eps, mu, std, z, B, SS, L, heads_np(2 * L));
+                     part, b_mu, b_lv, eps, mu, std, z, B, heads_ks(C, SS), L, heads_np(2 * L));
   if (launch_expand<0>(z, L, w_l2, nullptr, b_l2, dec_in, B, C, SS, L, L, st)) return 1;
   return evh::check_launch("heads_fwd");
 }
@@ -455,7 +475,8 @@ extern "C" int ebsdvae_latent_mu(const float* enc, const float* w_mu, const floa
   float* part = (float*)work;
   if (launch_partial<0>(enc, w_mu, nullptr, part, nullptr, 0, 0, B, C, SS, L, L, st)) return 1;
   hipLaunchKernelGGL(heads_fwd_finalize_kernel<true>, dim3((B * L + HT - 1) / HT), dim3(HT), 0, st,
-                     part, b_mu, nullptr, nullptr, mu, nullptr, nullptr, B, SS, L, heads_np(L));
+                     part, b_mu, nullptr, nullptr, mu, nullptr, nullptr, B, heads_ks(C, SS), L,
+                     heads_np(L));
   return evh::check_launch("latent_mu");
 }
 
@@ -473,7 +494,7 @@ extern "C" int ebsdvae_heads_bwd(const float* g_dec, const float* g_z, const flo
   // g_z partials (linear2 adjoint); g_out copied into gs in NCHW order for heads_wgrad
   if (launch_partial<1>(g_dec, w_l2, nullptr, part, gs, G, 2 * L, B, C, SS, L, L, st)) return 1;
   hipLaunchKernelGGL(heads_bwd_finalize_kernel, dim3((B * L + HT - 1) / HT), dim3(HT), 0, st, part,
-                     g_z, g_mu, g_std, std, eps, gs, B, SS, L, heads_np(L), G);
+                     g_z, g_mu, g_std, std, eps, gs, B, heads_ks(C, SS), L, heads_np(L), G);
   if (launch_expand<1>(gs, G, w_mu, w_lv, nullptr, g_enc, B, C, SS, L, 2 * L, st)) return 1;
   return evh::check_launch("heads_bwd");
 }
