@@ -372,6 +372,14 @@ EV_DEVINL void pipe_barrier() {
 //         column (pipe_prefetch_ok), PH 1 only loads the tile's y_prev values into pv (issued
 //         one iteration early, so their latency hides under that iteration's MFMAs) and PH 2
 //         is the epilogue reading them from pv instead of memory (same values, same order)
+// cache policy of the epilogue's stream traffic -- the output stores and the fused reduce's
+// y_prev loads, each touched once -- non-temporal (CPol NT), so the L2 keeps the halo lines the
+// next chunk iterations and tiles re-read instead
+#ifndef EV_EPI_POL
+#define EV_EPI_POL 2
+#endif
+constexpr int kEpiPol = EV_EPI_POL;
+
 template <int MF, int NF, int FP>
 constexpr bool pipe_prefetch_ok() { return NF == 1 && (FP == P_ID || FP == FP_UPSUM); }
 template <int MF, int NF, int FP>
@@ -414,7 +422,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
             pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
           }
           pv[g * 8 + k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                        rp, ((prow * W2 + pc) * NT + co) * 4, 0, 0));
+                                                        rp, ((prow * W2 + pc) * NT + co) * 4, 0, kEpiPol));
         }
       }
     } else {
@@ -428,7 +436,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
         const int mf = e >> 4, r = e & 15;
         const int pl = pbase + mf * 32 + (r & 3) + 8 * (r >> 2);
         pv[e] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(rp, (inbwd_pix<FP>(pl, W, lW, 0) * NT + co) * 4, 0, 0));
+            float, __builtin_amdgcn_raw_buffer_load_b32(rp, (inbwd_pix<FP>(pl, W, lW, 0) * NT + co) * 4, 0, kEpiPol));
       }
     }
     (void)nf;
@@ -466,7 +474,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
           // element 0 -- hipcc / ROCm 7.2)
           const float v = acc[mf][nf][r];
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
-                                                vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
+                                                vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, kEpiPol);
         }
     }
     if (FP == FP_UPSUM) {
@@ -504,12 +512,12 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           v[k] = PH == 2 ? pv[g * 8 + k]
-                         : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, 0));
+                         : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, off[k], 0, kEpiPol));
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float h = inbwd_acc<P_ID>(gs[k], &v[k], sp, spc, s1, s2);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), rq, off[k], 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), rq, off[k], 0, kEpiPol);
         }
         s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 32, 64);
@@ -532,7 +540,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
                                   fmaxf(acc[m0 + 1][nf][r], acc[m0 + 1][nf][r + 1]));
             const int pc = pcol + (((r & 3) + 8 * (r >> 2)) >> 1);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
-                                                  ((prow * W2 + pc) * NT + co) * 4, 0, 0);
+                                                  ((prow * W2 + pc) * NT + co) * 4, 0, kEpiPol);
           }
         } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
 #pragma unroll
@@ -544,7 +552,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
                                     fmaxf(acc[mf][nf][r + 8], acc[mf][nf][r + 9]));
               const int pc = ((r & 3) + 8 * (r >> 2) + 4 * hk) >> 1;
               __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
-                                                    ((prow * W2 + pc) * NT + co) * 4, 0, 0);
+                                                    ((prow * W2 + pc) * NT + co) * 4, 0, kEpiPol);
             }
           }
         }
@@ -576,14 +584,14 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
             for (int k = 0; k < NL; ++k)
               v[j][k] = PH == 2 ? pv[e]
                                 : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                rp, (inbwd_pix<FP>(pl, W, lW, k) * NT + co) * 4, 0, 0));
+                                                                rp, (inbwd_pix<FP>(pl, W, lW, k) * NT + co) * 4, 0, kEpiPol));
           }
 #pragma unroll
           for (int j = 0; j < G; ++j) {
             const int e = e0 + j, mf = e >> 4, r = e & 15;
             const float h = inbwd_acc<FP>(acc[mf][nf][r], v[j], sp, spc, s1, s2);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), ry,
-                                                  vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, 0);
+                                                  vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, kEpiPol);
           }
         }
         s1 += __shfl_xor(s1, 32, 64);
