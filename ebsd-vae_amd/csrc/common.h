@@ -45,6 +45,16 @@ EV_DEVINL float2 norm_fs(float2 st) { return make_float2(st.y, -st.x * st.y); }
 EV_DEVINL float normact_fs(float v, float2 fs) { return lrelu(fmaf(v, fs.x, fs.y)); }
 
 EV_DEVINL float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// non-temporal (CPol NT) forms for single-use stream traffic, so the L2 keeps what other
+// kernels re-read
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+EV_DEVINL float4 ld4_nt(const float* p) {
+  const f32v4 v = __builtin_nontemporal_load(reinterpret_cast<const f32v4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+EV_DEVINL void st4_nt(float* p, float4 v) {
+  __builtin_nontemporal_store(f32v4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32v4*>(p));
+}
 
 // The first conv (1 -> C, latice/model.py:110) at one pixel and one output channel: nb[t] =
 // x[h + t/3 - 1][w + t%3 - 1] (0 outside the image), wt = the channel's 9 taps.  One fixed fma

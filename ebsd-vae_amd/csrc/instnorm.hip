@@ -105,13 +105,13 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
 #pragma unroll 2
     for (int q = q0 + pr; q < q1; q += NPR) {
       const int h2 = q / W2, w2 = q - h2 * W2;
-      const float4 g4 = ld4(gnb + (size_t)q * C + c);
+      const float4 g4 = APPLY ? ld4_nt(gnb + (size_t)q * C + c) : ld4(gnb + (size_t)q * C + c);
       const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
       const size_t p00 = ((size_t)(2 * h2) * W + 2 * w2) * C + c;
       const size_t poff[4] = {p00, p00 + C, p00 + (size_t)W * C, p00 + (size_t)W * C + C};
       float4 yv[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) yv[k] = ld4(yb + poff[k]);
+      for (int k = 0; k < 4; ++k) yv[k] = APPLY ? ld4_nt(yb + poff[k]) : ld4(yb + poff[k]);
       float xh[4][4];  // [window slot][channel]
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
     for (int p = p0 + pr; p < p1; p += NPR) {
       float4 g4;
       if (pmode == P_ID) {
-        g4 = ld4(gnext + ((size_t)b * H * W + p) * C + c);
+        g4 = APPLY ? ld4_nt(gnext + ((size_t)b * H * W + p) * C + c) : ld4(gnext + ((size_t)b * H * W + p) * C + c);
       } else {  // P_UP: gnext at (2H, 2W)
         const int h = p / W, w = p - h * W;
         const float* s = gnext + (((size_t)b * 2 * H + 2 * h) * 2 * W + 2 * w) * C + c;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(
         g4 = make_float4(u0.x + u1.x + u2.x + u3.x, u0.y + u1.y + u2.y + u3.y,
                          u0.z + u1.z + u2.z + u3.z, u0.w + u1.w + u2.w + u3.w);
       }
-      const float4 y4 = ld4(yb + (size_t)p * C + c);
+      const float4 y4 = APPLY ? ld4_nt(yb + (size_t)p * C + c) : ld4(yb + (size_t)p * C + c);
       const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
       const float yy[4] = {y4.x, y4.y, y4.z, y4.w};
       float o[4];
@@ -325,11 +325,13 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
   constexpr bool PF = !(FUSE_ == FUSE_FINAL && !APPLY);
   constexpr int U = PF ? 4 : 2;
   constexpr bool LG = FUSE_ == FUSE_FIRST;
+  // single-use stream reads: non-temporal (the reduce-only FINAL pass keeps the default)
   auto ldy = [&](int p) {
-    return (!RC && p < p1) ? ld4(yb + (size_t)p * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    return (!RC && p < p1) ? (APPLY ? ld4_nt(yb + (size_t)p * C + c) : ld4(yb + (size_t)p * C + c))
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   auto ldg = [&](int p) {
-    return (LG && p < p1) ? ld4(gsrc + ((size_t)b * H * W + p) * C + c)
+    return (LG && p < p1) ? ld4_nt(gsrc + ((size_t)b * H * W + p) * C + c)
                           : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   float4 ycur[U], gcur[U];
