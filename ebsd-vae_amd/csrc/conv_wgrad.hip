@@ -495,8 +495,9 @@ EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[2][9], const double (&bs)[4], cha
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + wco * 32 + f * 16 + (lane >> 4) * 4 + r;
-          wpart[(((size_t)slice * 9 + tap) * Cout + co) * Cin + ci] =
-              F16 ? acc[f][tap][r] * (1.f / gsc) : acc[f][tap][r];
+          // the slice partials are read once, by the batched reduction: non-temporal
+          __builtin_nontemporal_store(F16 ? acc[f][tap][r] * (1.f / gsc) : acc[f][tap][r],
+                                      wpart + (((size_t)slice * 9 + tap) * Cout + co) * Cin + ci);
         }
   }
   if (do_bias) {
@@ -1191,7 +1192,7 @@ __global__ void wgrad_reduce1_batch_kernel(const WgReduceBatch rb, double* __res
   double s = 0.0;
   if (e < nw) {
 #pragma unroll 8
-    for (int k = k0; k < k1; ++k) s += (double)q.wpart[(size_t)k * nw + e];
+    for (int k = k0; k < k1; ++k) s += (double)__builtin_nontemporal_load(q.wpart + (size_t)k * nw + e);
   } else {
     const int co = e - nw;
     for (int k = k0; k < k1; ++k) s += (double)q.bpart[(size_t)k * q.cout + co];
