@@ -20,11 +20,16 @@
 // for the band's own rows).  The sums are fp32 per row and thread, double across rows, lanes
 // and waves (fixed order), as the reduce kernel it replaces.
 #include "common.h"
+
+#include <type_traits>
 #include "../../include/ebsdvae.h"
 
 namespace ev {
 
-constexpr int NE_C = 32, NE_TH = 16;
+constexpr int NE_C = 32;
+// rows per band: 32 where H allows (the two recomputed halo rows above and below cost 4 / TH of
+// the band's work), else 16
+__host__ __device__ constexpr int ne_th(int H) { return H % 32 == 0 ? 32 : 16; }
 constexpr int NE_RING = 4;                 // ring slots (a and g1): slot(row) = (row - r0 + k) & 3
 // per width: threads, ring row (zero column, W pixels, zero column), floats per a-ring row
 template <int W> constexpr int ne_nth() { return 2 * W; }
@@ -34,14 +39,10 @@ template <int W> constexpr size_t ne_lds() {
   return (size_t)(NE_RING * ne_arow<W>() + NE_RING * ne_wp<W>()) * sizeof(float);
 }
 
-EV_DEVINL float ne_bce(float xh, float t) {
-  return (1.f - t) * xh + fmaxf(-xh, 0.f) + log1pf(expf(-fabsf(xh)));
-}
-EV_DEVINL float ne_sigmoid(float x) {
-  if (x >= 0.f) return 1.f / (1.f + expf(-x));
-  const float e = expf(x);
-  return e / (1.f + e);
-}
+// BCE-with-logits term and sigmoid from one e = exp(-|x|) and one division: the same values as
+//   (1 - t) x + max(-x, 0) + log1p(exp(-|x|))  and  x >= 0 ? 1 / (1 + exp(-x)) : exp(x) / (1 + exp(x))
+EV_DEVINL float ne_bce_e(float xh, float t, float e) { return (1.f - t) * xh + fmaxf(-xh, 0.f) + log1pf(e); }
+EV_DEVINL float ne_sigmoid_e(float x, float e) { return (x >= 0.f ? 1.f : e) / (1.f + e); }
 // sum over the 8 channel-group lanes of a pixel (lanes 8k .. 8k+7), on the VALU through DPP:
 // quad_perm [1,0,3,2] (xor 1), [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7 - i,
 // which pairs the two quads of the 8-lane group)
@@ -56,13 +57,13 @@ EV_DEVINL float ne_fold8(float v) {
   return v;
 }
 
-template <int W>
+template <int W, int TH>
 __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
     const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
     const float* __restrict__ b14, const float* __restrict__ xt, const float* __restrict__ g_loss,
     float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
-  constexpr int C = NE_C, TH = NE_TH, WP = ne_wp<W>(), NE_AROW = ne_arow<W>();
+  constexpr int C = NE_C, WP = ne_wp<W>(), NE_AROW = ne_arow<W>();
   constexpr int NE_NTH = ne_nth<W>(), NPL = W / 4, NWAVE = NE_NTH / 64;
   extern __shared__ __attribute__((aligned(16))) float ne_sm[];
   float* aring = ne_sm;                       // [4][WP][C]
@@ -76,6 +77,8 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
   float2 fs[4];   // {rstd, -mean * rstd}
 #pragma unroll
   for (int k = 0; k < 4; ++k) fs[k] = norm_fs(st[(size_t)b * C + c + k]);
+  const pkf2 fsr[2] = {pk2(fs[0].x, fs[1].x), pk2(fs[2].x, fs[3].x)};   // rstd pairs
+  const pkf2 fsb[2] = {pk2(fs[0].y, fs[1].y), pk2(fs[2].y, fs[3].y)};   // -mean * rstd pairs
   pkf2 wv2[2][9];   // w14 (1, 32, 3, 3) as channel pairs (c, c+1), (c+2, c+3)
 #pragma unroll
   for (int k = 0; k < 2; ++k)
@@ -128,14 +131,19 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
     // (1) a = lrelu(IN(y13)) of source row q into ring slot i & 3 (zero outside the image)
     {
       float* ar = aring + (i & 3) * NE_AROW;
-      const bool in = q >= 0 && q < H;
+      if (q >= 0 && q < H) {   // block-uniform
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float4 v = ycur[j];
-        v = make_float4(normact_fs(v.x, fs[0]), normact_fs(v.y, fs[1]), normact_fs(v.z, fs[2]),
-                        normact_fs(v.w, fs[3]));
-        if (!in) v = make_float4(0.f, 0.f, 0.f, 0.f);
-        st4(ar + (pl + NPL * j + 1) * C + c, v);
+        for (int j = 0; j < 4; ++j) {
+          // normact_fs per value, two channels per packed fma / mul
+          const float4 v = ycur[j];
+          const pkf2 u0 = pkfma(pk2(v.x, v.y), fsr[0], fsb[0]), u1 = pkfma(pk2(v.z, v.w), fsr[1], fsb[1]);
+          const pkf2 k0 = u0 * pk2(kSlope, kSlope), k1 = u1 * pk2(kSlope, kSlope);
+          st4(ar + (pl + NPL * j + 1) * C + c,
+              make_float4(fmaxf(u0.x, k0.x), fmaxf(u0.y, k0.y), fmaxf(u1.x, k1.x), fmaxf(u1.y, k1.y)));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st4(ar + (pl + NPL * j + 1) * C + c, make_float4(0.f, 0.f, 0.f, 0.f));
       }
     }
     // prefetch row q + 2 into the registers just consumed
@@ -168,11 +176,12 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
         const int w = pl + NPL * cg;
         float g = 0.f;
         if (inrow) {
-          g = cr * (ne_sigmoid(xsel) - tcur);
+          const float e = expf(-fabsf(xsel));
+          g = cr * (ne_sigmoid_e(xsel, e) - tcur);
           if (own) {
             x_hat[(size_t)b * HW + (size_t)r * W + w] = xsel;
             g1out[(size_t)b * HW + (size_t)r * W + w] = g;
-            bce += ne_bce(xsel, tcur);
+            bce += ne_bce_e(xsel, tcur, e);
             bsum += g;
           }
         }
@@ -189,7 +198,7 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
       const float* gB = gring + ((i - 1) & 3) * WP;        // row q - 2
       const float* gC = gring + (i & 3) * WP;              // row q - 1
       const float* am = aring + ((i - 2) & 3) * NE_AROW;   // a of row q - 2
-      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+      pkf2 s1[2] = {pk2(0.f, 0.f), pk2(0.f, 0.f)}, s2[2] = {pk2(0.f, 0.f), pk2(0.f, 0.f)};
 #pragma unroll 2
       for (int j = 0; j < 4; ++j) {
         const int w = pl + NPL * j;
@@ -211,14 +220,17 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
         }
         const float4 a4 = ld4(am + (w + 1) * C + c);
         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-        const float gav[4] = {ga[0].x, ga[0].y, ga[1].x, ga[1].y};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          // xhat from a = lrelu(xhat): exact sign, |error| ~ 1 ulp on the negative side
-          const float xh = av[k] > 0.f ? av[k] : av[k] * (1.f / kSlope);
-          const float gx = gav[k] * slope(xh);
+        for (int k = 0; k < 2; ++k) {
+          // xhat from a = lrelu(xhat): exact sign (xhat > 0 iff a > 0), |error| ~ 1 ulp on the
+          // negative side; gx = g_a * lrelu'(xhat)
+          const pkf2 a2 = pk2(av[2 * k], av[2 * k + 1]);
+          const pkf2 xs = a2 * pk2(1.f / kSlope, 1.f / kSlope);
+          const bool p0 = a2.x > 0.f, p1 = a2.y > 0.f;
+          const pkf2 xh = pk2(p0 ? a2.x : xs.x, p1 ? a2.y : xs.y);
+          const pkf2 gx = ga[k] * pk2(p0 ? 1.f : kSlope, p1 ? 1.f : kSlope);
           s1[k] += gx;
-          s2[k] = fmaf(gx, xh, s2[k]);
+          s2[k] = pkfma(gx, xh, s2[k]);
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -228,7 +240,10 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
         }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { s1d[k] += (double)s1[k]; s2d[k] += (double)s2[k]; }
+      for (int k = 0; k < 4; ++k) {
+        s1d[k] += (double)((k & 1) ? s1[k >> 1].y : s1[k >> 1].x);
+        s2d[k] += (double)((k & 1) ? s2[k >> 1].y : s2[k >> 1].x);
+      }
     }
   };
 #pragma unroll 1
@@ -300,21 +315,22 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
 using namespace ev;
 
 extern "C" int ebsdvae_net_end_tiles(int H, int W) {
-  return ((W == 128 || W == 256) && ev_dim_ok(H) && H % NE_TH == 0) ? H / NE_TH : -1;
+  return ((W == 128 || W == 256) && ev_dim_ok(H) && H % 16 == 0) ? H / ne_th(H) : -1;
 }
 
-template <int W>
+template <int W, int TH>
 static void net_end_launch(dim3 grid, hipStream_t st, const float* y13, const float* st13,
                            const float* w14, const float* b14, const float* x, const float* g_loss,
                            float gscale, float* x_hat, float* g1, float* bce_part, double* part,
                            float* wpart, float* bpart, int H) {
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)net_end_kernel<W>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)(net_end_kernel<W, TH>), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)ne_lds<W>());
     once = true;
   }
-  hipLaunchKernelGGL(net_end_kernel<W>, grid, dim3(ne_nth<W>()), ne_lds<W>(), st, y13,
+  auto k = net_end_kernel<W, TH>;
+  hipLaunchKernelGGL(k, grid, dim3(ne_nth<W>()), ne_lds<W>(), st, y13,
                      (const float2*)st13, w14, b14, x, g_loss, gscale, x_hat, g1, bce_part,
                      (double2*)part, wpart, bpart, H);
 }
@@ -326,14 +342,19 @@ extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float*
   EV_REQUIRE(y13 && st13 && w14 && x && x_hat && g1 && bce_part && part && wpart && bpart && B > 0,
              "net_end: null pointer");
   EV_REQUIRE(C == NE_C && ebsdvae_net_end_tiles(H, W) > 0,
-             "net_end: C=%d %dx%d unsupported (C 32, W 128 or 256, H a multiple of %d)", C, H, W, NE_TH);
-  const int T = H / NE_TH;
+             "net_end: C=%d %dx%d unsupported (C 32, W 128 or 256, H a multiple of 16)", C, H, W);
+  const int T = ebsdvae_net_end_tiles(H, W);
   const float gscale = scale / ((float)B * (float)(H * W));
-  if (W == 128)
-    net_end_launch<128>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
-                        g1, bce_part, part, wpart, bpart, H);
-  else
-    net_end_launch<256>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
-                        g1, bce_part, part, wpart, bpart, H);
+  auto go = [&](auto w_c, auto th_c) {
+    net_end_launch<decltype(w_c)::value, decltype(th_c)::value>(dim3(T, B), (hipStream_t)stream, y13, st13, w14,
+                                                                b14, x, g_loss, gscale, x_hat, g1, bce_part,
+                                                                part, wpart, bpart, H);
+  };
+  using I128 = std::integral_constant<int, 128>;
+  using I256 = std::integral_constant<int, 256>;
+  using T16 = std::integral_constant<int, 16>;
+  using T32 = std::integral_constant<int, 32>;
+  if (W == 128) { if (ne_th(H) == 32) go(I128{}, T32{}); else go(I128{}, T16{}); }
+  else { if (ne_th(H) == 32) go(I256{}, T32{}); else go(I256{}, T16{}); }
   return evh::check_launch("net_end");
 }
