@@ -34,6 +34,8 @@ CASES = {
     "fwd32to64n": ("fwd", 64, 32, 64, ACT_NORM),
     "fwd128s8": ("fwd", 8, 128, 128, ACT_NORM),
     "dgrad128s8": ("dgrad", 8, 128, 128, P_ID),
+    "fwd128s16": ("fwd", 16, 128, 128, ACT_NORM),
+    "dgrad128s16": ("dgrad", 16, 128, 128, P_ID),
     "dgrad32": ("dgrad", 128, 32, 32, P_ID),
     "dgrad64": ("dgrad", 64, 64, 64, P_ID),
     "dgrad32u": ("dgrad", 128, 32, 32, P_UP),
