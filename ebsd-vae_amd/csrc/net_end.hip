@@ -20,16 +20,12 @@
 // for the band's own rows).  The sums are fp32 per row and thread, double across rows, lanes
 // and waves (fixed order), as the reduce kernel it replaces.
 #include "common.h"
-
-#include <type_traits>
 #include "../../include/ebsdvae.h"
 
 namespace ev {
 
-constexpr int NE_C = 32;
-// rows per band: 32 where H allows (the two recomputed halo rows above and below cost 4 / TH of
-// the band's work), else 16
-__host__ __device__ constexpr int ne_th(int H) { return H % 32 == 0 ? 32 : 16; }
+// rows per band: the two recomputed halo rows above and below cost 4 / TH of the band's work
+constexpr int NE_C = 32, NE_TH = 32;
 constexpr int NE_RING = 4;                 // ring slots (a and g1): slot(row) = (row - r0 + k) & 3
 // per width: threads, ring row (zero column, W pixels, zero column), floats per a-ring row
 template <int W> constexpr int ne_nth() { return 2 * W; }
@@ -57,13 +53,13 @@ EV_DEVINL float ne_fold8(float v) {
   return v;
 }
 
-template <int W, int TH>
+template <int W>
 __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
     const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
     const float* __restrict__ b14, const float* __restrict__ xt, const float* __restrict__ g_loss,
     float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
-  constexpr int C = NE_C, WP = ne_wp<W>(), NE_AROW = ne_arow<W>();
+  constexpr int C = NE_C, TH = NE_TH, WP = ne_wp<W>(), NE_AROW = ne_arow<W>();
   constexpr int NE_NTH = ne_nth<W>(), NPL = W / 4, NWAVE = NE_NTH / 64;
   extern __shared__ __attribute__((aligned(16))) float ne_sm[];
   float* aring = ne_sm;                       // [4][WP][C]
@@ -315,21 +311,21 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
 using namespace ev;
 
 extern "C" int ebsdvae_net_end_tiles(int H, int W) {
-  return ((W == 128 || W == 256) && ev_dim_ok(H) && H % 16 == 0) ? H / ne_th(H) : -1;
+  return ((W == 128 || W == 256) && ev_dim_ok(H) && H % NE_TH == 0) ? H / NE_TH : -1;
 }
 
-template <int W, int TH>
+template <int W>
 static void net_end_launch(dim3 grid, hipStream_t st, const float* y13, const float* st13,
                            const float* w14, const float* b14, const float* x, const float* g_loss,
                            float gscale, float* x_hat, float* g1, float* bce_part, double* part,
                            float* wpart, float* bpart, int H) {
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)(net_end_kernel<W, TH>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)(net_end_kernel<W>), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)ne_lds<W>());
     once = true;
   }
-  auto k = net_end_kernel<W, TH>;
+  auto k = net_end_kernel<W>;
   hipLaunchKernelGGL(k, grid, dim3(ne_nth<W>()), ne_lds<W>(), st, y13,
                      (const float2*)st13, w14, b14, x, g_loss, gscale, x_hat, g1, bce_part,
                      (double2*)part, wpart, bpart, H);
@@ -342,19 +338,14 @@ extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float*
   EV_REQUIRE(y13 && st13 && w14 && x && x_hat && g1 && bce_part && part && wpart && bpart && B > 0,
              "net_end: null pointer");
   EV_REQUIRE(C == NE_C && ebsdvae_net_end_tiles(H, W) > 0,
-             "net_end: C=%d %dx%d unsupported (C 32, W 128 or 256, H a multiple of 16)", C, H, W);
+             "net_end: C=%d %dx%d unsupported (C 32, W 128 or 256, H a multiple of %d)", C, H, W, NE_TH);
   const int T = ebsdvae_net_end_tiles(H, W);
   const float gscale = scale / ((float)B * (float)(H * W));
-  auto go = [&](auto w_c, auto th_c) {
-    net_end_launch<decltype(w_c)::value, decltype(th_c)::value>(dim3(T, B), (hipStream_t)stream, y13, st13, w14,
-                                                                b14, x, g_loss, gscale, x_hat, g1, bce_part,
-                                                                part, wpart, bpart, H);
-  };
-  using I128 = std::integral_constant<int, 128>;
-  using I256 = std::integral_constant<int, 256>;
-  using T16 = std::integral_constant<int, 16>;
-  using T32 = std::integral_constant<int, 32>;
-  if (W == 128) { if (ne_th(H) == 32) go(I128{}, T32{}); else go(I128{}, T16{}); }
-  else { if (ne_th(H) == 32) go(I256{}, T32{}); else go(I256{}, T16{}); }
+  if (W == 128)
+    net_end_launch<128>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
+                        g1, bce_part, part, wpart, bpart, H);
+  else
+    net_end_launch<256>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
+                        g1, bce_part, part, wpart, bpart, H);
   return evh::check_launch("net_end");
 }
