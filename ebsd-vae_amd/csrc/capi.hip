@@ -30,7 +30,9 @@ int check_launch(const char* what) {
 }  // namespace evh
 
 extern "C" const char* ebsdvae_last_error(void) { return g_err; }
-extern "C" int ebsdvae_version(void) { return 1; }
+// ABI version (include/ebsdvae.h EBSDVAE_ABI_VERSION): 2 since the heads entry points took
+// their caller-owned `work` scratch (round 4); latice/_native.load() refuses any other value
+extern "C" int ebsdvae_version(void) { return EBSDVAE_ABI_VERSION; }
 
 // ------------------------------------------------------------------ cross-stream ordering
 // `waiter` waits for the work enqueued on `signaler` so far, through an event recorded with a

@@ -110,6 +110,9 @@ QUERIES = {"ebsdvae_version", "ebsdvae_conv_first_stat_tiles", "ebsdvae_conv3x3_
            "ebsdvae_conv3x3_split_pool_ok",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices", "ebsdvae_net_end_tiles"}
 
+# include/ebsdvae.h EBSDVAE_ABI_VERSION: the signatures above
+ABI_VERSION = 2
+
 _lib = None
 _lock = threading.Lock()
 
@@ -156,6 +159,11 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        v = lib.ebsdvae_version()
+        if v != ABI_VERSION:
+            raise NativeLibraryError(
+                f"{p} implements C ABI version {v}, this binding needs {ABI_VERSION} "
+                "(include/ebsdvae.h EBSDVAE_ABI_VERSION): rebuild it with `python ebsd-vae_amd/build.py`")
         if path is None:
             _lib = lib
         return lib

@@ -11,6 +11,12 @@ from __future__ import annotations
 import torch
 from torch.utils._pytree import tree_map
 
+class StaleDeferredError(RuntimeError):
+    """A deferred value whose inputs changed before it was first computed: it can no longer be
+    computed as the call that made it would have returned it.  Raised by the thunk (model.py)
+    and, on every later read, again by materialize()."""
+
+
 _T = torch.Tensor
 # metadata queries answered by the wrapper itself, without computing the value
 _META = {_T.shape.__get__, _T.dtype.__get__, _T.device.__get__, _T.size, _T.dim,

@@ -229,9 +229,12 @@ def defer_until_weights_change(t) -> None:
 def before_weights_write() -> None:
     """Materialise every pending deferred value (called before a fused optimizer step or a
     graph replay writes parameters through raw pointers).  A value that can no longer be
-    computed (its parameters already changed through torch) is left to raise where it is read,
-    not here: the weight writer is not the call site at fault.  Nothing runs while a stream is
-    being captured (the decoder launches would land in the graph)."""
+    computed (its parameters already changed through torch: StaleDeferredError) is left to
+    raise where it is read, not here: the weight writer is not the call site at fault.  Any
+    other failure (a launch error, out of memory) propagates from here, before the weights
+    change.  Nothing runs while a stream is being captured (the decoder launches would land
+    in the graph)."""
+    from .deferred import StaleDeferredError
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         return
     while _PENDING:
@@ -240,7 +243,7 @@ def before_weights_write() -> None:
         if t is not None:
             try:
                 t.materialize()
-            except RuntimeError:
+            except StaleDeferredError:
                 pass   # materialize() keeps the thunk: the first read raises the same error
 
 

@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 
 from . import engine as E
-from .deferred import DeferredTensor
+from .deferred import DeferredTensor, StaleDeferredError
 from .functional import DecoderFn, EncoderFn, HeadsFn, LinearFn, ReparamFn
 
 # EBSDVAE_DEFER_DECODE=0: the eval/no-grad forward runs the decoder eagerly (A/B timing)
@@ -148,8 +148,8 @@ class VariationalAutoEncoder(nn.Module):
             # raw-pointer weight writers materialise pending values first
             # (engine.before_weights_write); a torch in-place update bumps _version
             if gen != E.weights_generation() or any(p._version != v for p, v in versions):
-                raise RuntimeError("model parameters changed between model(x) and the first use "
-                                   "of its deferred x_hat")
+                raise StaleDeferredError("model parameters changed between model(x) and the first "
+                                         "use of its deferred x_hat")
             cur = torch.cuda.current_stream(x.device)
             if cur != made_on:
                 cur.wait_event(ready)

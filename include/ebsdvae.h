@@ -36,6 +36,10 @@ extern "C" {
 typedef void* ebsdvae_stream_t; /* hipStream_t */
 
 const char* ebsdvae_last_error(void);
+/* ABI version of this header; ebsdvae_version() returns the library's.  Bumped on every
+ * incompatible signature change (2: ebsdvae_heads_fwd / _bwd / ebsdvae_latent_mu take a
+ * caller-owned `work` scratch pointer).  Callers must check it before the first call. */
+#define EBSDVAE_ABI_VERSION 2
 int ebsdvae_version(void);
 
 /* ---- stream ordering ------------------------------------------------------------------

@@ -21,7 +21,7 @@ static void expect_err(int rc, const char* what) {
 }
 
 int main() {
-  if (ebsdvae_version() != 1) { printf("FAIL version\n"); return 1; }
+  if (ebsdvae_version() != EBSDVAE_ABI_VERSION) { printf("FAIL version\n"); return 1; }
   const int sizes[] = {-8, 0, 1, 4, 7, 8, 16, 32, 64, 100, 128, 256, 512, 4096, 1 << 20};
   const int chans[] = {-1, 0, 1, 3, 8, 16, 32, 64, 96, 128, 256};
   const int pieces[] = {-1, 0, 1, 2, 3, EBSDVAE_PIECES_F16, 99};

@@ -35,11 +35,14 @@ ZERO_GRAD_BIAS = tuple(f"encoder.{i}.0.bias" for i in O.ENC_IDX) + tuple(
     f"decoder.{i}.0.bias" for i in O.DEC_IDX)
 DECISION_GATE = 1e-3
 STATE_GATE = 1e-4
-# residue gate, in units of 2^-24 * A_c (<= 6.1e-5 of sum |gy|).  Measured on MI355X (round 4,
-# every fixture, B = 4..256, all arithmetics and switches): f16x3 <= 3.0, bf16x6 <= 1.7, fp32
-# <= 181 (decoder.13.0 on vae128_b8_c1: the fp32 weight-gradient kernel's longer sequential
-# slice sums); the reference's own fp32 run at B = 256: 0.18 (bias_noise_b256.npz)
-ZERO_BIAS_K = 1024.0
+# residue gate, in units of 2^-24 * A_c, per conv arithmetic (the one in effect when check_grads
+# runs).  Measured on MI355X (round 4, every fixture, B = 4..256, every switch): f16x3 <= 3.0,
+# bf16x6 <= 1.7, fp32 <= 1.4 -- save ONE fp32 run of 180.8 on decoder.13.0 (vae128_b8_c1,
+# gpurun_out/t_sw1.txt) whose other runs of the same test read 0.6: a run-to-run difference,
+# not the arithmetic, which tests/test_gpu_determinism.py now looks for directly.  The
+# reference's own fp32 run at B = 256: 0.18 (bias_noise_b256.npz).  A 16x margin over the
+# worst measured value of every arithmetic.
+ZERO_BIAS_K = {"f16x3": 16.0, "bf16x6": 16.0, "bf16x3": 16.0, "fp32": 16.0}
 U32 = 2.0 ** -24
 
 
@@ -70,8 +73,12 @@ def blocks(plan, rec):
     return [one(L) for L in plan.enc], [one(L) for L in plan.dec]
 
 
-def check_grads(name, plan, rec, grads, label=""):
-    """grads: {state_dict name: GPU gradient tensor}.  Prints every error, then asserts."""
+def check_grads(name, plan, rec, grads, label="", prec=None):
+    """grads: {state_dict name: GPU gradient tensor}; prec: the conv arithmetic that computed
+    them (default: the one in effect now).  Prints every error, then asserts."""
+    from latice import engine as E
+    prec = prec or E.get_precision()
+    kz = ZERO_BIAS_K[prec]
     f, sd = fixture(name)
     kl = float(f["kl_lambda"])
     enc_b, dec_b = blocks(plan, rec)
@@ -87,7 +94,7 @@ def check_grads(name, plan, rec, grads, label=""):
             # residue in units of 2^-24 * A_c, worst channel
             a = float((np.abs(g) / (U32 * np.maximum(absum[n], 1e-300))).max())
             rows.append((n, a, None))
-            if a > ZERO_BIAS_K:
+            if a > kz:
                 fails.append((n, "zero-bias", a))
             continue
         es, ed = O.rel_err(g, g_state[n]), O.rel_err(g, g_dec[n])
@@ -100,7 +107,8 @@ def check_grads(name, plan, rec, grads, label=""):
     worst_d = max(r[2] for r in rows if r[2] is not None)
     worst_b = max(r[1] for r in rows if r[2] is None)
     print(f"\n[{label} {name}] worst weight-grad err: state-pinned {worst_s:.2e}, "
-          f"decision-pinned {worst_d:.2e}; worst zero-grad bias residue {worst_b:.1f} x 2^-24 A")
+          f"decision-pinned {worst_d:.2e}; worst zero-grad bias residue {worst_b:.1f} x 2^-24 A "
+          f"(gate {kz:g}, {prec})")
     for n, a, b in rows:
         print(f"    {n:22s} " + (f"residue {a:.1f} x 2^-24 A" if b is None else f"state {a:.2e}  decision {b:.2e}"))
     assert not fails, fails

@@ -42,7 +42,7 @@ def main():
         assert err <= 1e-5, f"{prec}: loss rel err {err:.2e}"
         rec0 = {n: (y[:b], st[:b]) for n, (y, st) in rec.items()}
         switches = {k: v for k, v in os.environ.items() if k.startswith("EBSDVAE_")}
-        check_grads(name, m.plan, rec0, tr.G, label=f"{switches} {prec} B={b * copies}")
+        check_grads(name, m.plan, rec0, tr.G, label=f"{switches} {prec} B={b * copies}", prec=prec)
     print("switch child OK")
 
 

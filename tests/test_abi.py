@@ -40,11 +40,18 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
 
 
+def header_abi_version() -> int:
+    """EBSDVAE_ABI_VERSION of include/ebsdvae.h (the binding's ABI_VERSION must equal it)."""
+    m = re.search(r"#define\s+EBSDVAE_ABI_VERSION\s+(\d+)", open(HEADER).read())
+    assert m, "include/ebsdvae.h defines EBSDVAE_ABI_VERSION"
+    return int(m.group(1))
+
+
 def test_library_loads_and_binds():
     _ensure_built()
     from latice import _native
     lib = _native.load()
-    assert lib.ebsdvae_version() == 1
+    assert lib.ebsdvae_version() == _native.ABI_VERSION == header_abi_version()
     for name in _native.exported_symbols():
         assert hasattr(lib, name)
     # host-side shape queries run without a GPU

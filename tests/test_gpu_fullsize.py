@@ -13,7 +13,7 @@ of a fixture's (x, eps) goes through those paths and still has the fixture's ans
     BITWISE equal to copy 0's -- a size-dependent bug in tile ownership, slice partitioning
     or the finalize shows up as copies that differ;
   * the gradient is then checked exactly like the fixture-size tests (tests/pinned.py:
-    decision-pinned <= 1e-3, state-pinned <= 1e-4, zero-grad bias residues <= ZERO_BIAS_K x 2^-24 sum|gy|), with copy 0's
+    decision-pinned <= 1e-3, state-pinned <= 1e-4, zero-grad bias residues <= ZERO_BIAS_K[arithmetic] x 2^-24 sum|gy|), with copy 0's
     state as the pin.
 
 Configs (BASELINE.json): c2 = 128x128, latent 16, batch 256 through
@@ -76,7 +76,7 @@ def test_trainer_full_size_tiled_fixture(cuda, name, copies, prec):
               if not (_copies_identical(rec[L.name][0], b) and _copies_identical(rec[L.name][1], b))]
     assert not differ, f"copies of one pattern saved different forward state: {differ}"
     rec0 = {n: (y[:b], st[:b]) for n, (y, st) in rec.items()}
-    check_grads(name, m.plan, rec0, tr.G, label=f"trainer B={b * copies} {prec}")
+    check_grads(name, m.plan, rec0, tr.G, label=f"trainer B={b * copies} {prec}", prec=prec)
 
 
 @pytest.mark.parametrize("prec", ["f16x3", "fp32"])

@@ -259,11 +259,14 @@ def test_cout1_conv_fwd_dgrad_and_first_conv_input_grad(cuda):
     assert O.rel_err(host(gx)[:, 0], O.conv3x3_dgrad(gy, w0)[..., 0]) < TOL
 
 
+# B = 5: the one-pattern tiles; B = 300: two-pattern tiles with a partly filled last tile (the
+# b < B masks at R > 1); B = 1024: the c4 batch
+@pytest.mark.parametrize("B", [5, 300, 1024])
 @pytest.mark.parametrize("S,L", [(128, 16), (256, 64)])
-def test_heads_forward_backward(cuda, S, L):
-    rng = np.random.default_rng(S + L)
+def test_heads_forward_backward(cuda, S, L, B):
+    rng = np.random.default_rng(S + L + B)
     plan = E.build_plan(32, L, S)
-    B, s, C, F = 5, plan.enc_side, plan.enc_channels, plan.feat
+    s, C, F = plan.enc_side, plan.enc_channels, plan.feat
     enc = rng.standard_normal((B, s, s, C))
     p = {"mu.0.weight": rng.standard_normal((L, F)) * 0.02, "mu.0.bias": rng.standard_normal(L) * 0.1,
          "logvar.0.weight": rng.standard_normal((L, F)) * 0.02,
@@ -299,6 +302,12 @@ def test_heads_forward_backward(cuda, S, L):
         assert O.rel_err(host(grads[k]), v) < 1e-4, k
     rgenc = O.nchw_unflatten(gmt @ p["mu.0.weight"] + glv @ p["logvar.0.weight"], C, s)
     assert O.rel_err(host(g_enc), rgenc) < 1e-4
+    # the inference heads (encode_latents' ebsdvae_latent_mu) on the same features
+    mu2 = torch.empty(B, L, device="cuda")
+    work = E._heads_work(B, plan, mu2)
+    N.call("ebsdvae_latent_mu", N.ptr(dev(enc)), N.ptr(pd["mu.0.weight"]), N.ptr(pd["mu.0.bias"]),
+           N.ptr(mu2), N.ptr(work), B, C, s, L, N.stream())
+    assert O.rel_err(host(mu2), rmu) < 1e-5
 
 
 @pytest.mark.parametrize("B,P", [(4, 128 * 128), (3, 250)])

@@ -56,7 +56,7 @@ def test_autocast_fp16_gradscaler_step(cuda, prec):
     assert abs(float(losses["loss"]) - ref) <= 1e-5 * abs(ref)
     assert O.rel_err(host(x_hat), f["x_hat"]) < 1e-4
     grads = {n: p.grad for n, p in m.named_parameters()}
-    check_grads("vae128_b4", m.plan, rec, grads, label=f"autocast-f16 + GradScaler {prec}")
+    check_grads("vae128_b4", m.plan, rec, grads, label=f"autocast-f16 + GradScaler {prec}", prec=prec)
 
 
 def test_validation_step_under_inference_mode(cuda, monkeypatch):

@@ -76,7 +76,7 @@ def test_forward_loss_backward_vs_reference(cuda, name, prec):
         return
     losses["loss"].backward()
     grads = {n: p.grad for n, p in m.named_parameters()}
-    check_grads(name, m.plan, rec, grads, label=f"autograd {prec}")
+    check_grads(name, m.plan, rec, grads, label=f"autograd {prec}", prec=prec)
 
 
 def test_encoder_submodule_and_heads_direct_calls(cuda):

@@ -93,7 +93,7 @@ def test_arithmetic_switch_meets_pinned_gates(cuda, monkeypatch, switch, prec):
     f, m = _model(cuda)
     with E.precision(prec):
         tr, rec = _grad(m, f, cuda)
-    check_grads("vae128_b4", m.plan, rec, tr.G, label=f"{name}=0 {prec}")
+    check_grads("vae128_b4", m.plan, rec, tr.G, label=f"{name}=0 {prec}", prec=prec)
 
 
 def test_inference_switches_keep_outputs(cuda, monkeypatch):

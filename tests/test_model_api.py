@@ -106,10 +106,10 @@ def test_weight_writer_leaves_stale_deferred_values_to_their_reader():
     deferred values; one that can no longer be computed raises where it is read, not in the
     optimizer step that happened to flush it."""
     from latice import engine as E
-    from latice.deferred import DeferredTensor
+    from latice.deferred import DeferredTensor, StaleDeferredError
 
     def stale():
-        raise RuntimeError("model parameters changed between model(x) and the first use")
+        raise StaleDeferredError("model parameters changed between model(x) and the first use")
 
     good = DeferredTensor(lambda: torch.ones(2), (2,), torch.float32, torch.device("cpu"))
     bad = DeferredTensor(stale, (2,), torch.float32, torch.device("cpu"))
@@ -117,8 +117,31 @@ def test_weight_writer_leaves_stale_deferred_values_to_their_reader():
     E.defer_until_weights_change(good)
     E.before_weights_write()            # does not raise
     assert good.materialized and not bad.materialized and not E._PENDING
-    with pytest.raises(RuntimeError, match="parameters changed"):
+    with pytest.raises(StaleDeferredError, match="parameters changed"):
         bad.sum()
+
+
+def test_weight_writer_propagates_other_deferred_failures():
+    """Only the stale case is left to the reader: any other failure while flushing a
+    deferred value (a launch error, out of memory) propagates from the weight writer, before the
+    weights change, and the value stays computable afterwards."""
+    from latice import engine as E
+    from latice.deferred import DeferredTensor
+
+    calls = []
+
+    def flaky():
+        calls.append(1)
+        if len(calls) == 1:
+            raise RuntimeError("ebsdvae_conv3x3_fwd_split_st failed (1): out of memory")
+        return torch.full((2,), 3.0)
+
+    d = DeferredTensor(flaky, (2,), torch.float32, torch.device("cpu"))
+    E.defer_until_weights_change(d)
+    with pytest.raises(RuntimeError, match="out of memory"):
+        E.before_weights_write()
+    assert not d.materialized
+    assert float(d.sum()) == 6.0 and d.materialized
 
 
 def test_datamodule_split_matches_random_split(tmp_path):

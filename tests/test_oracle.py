@@ -93,8 +93,13 @@ def test_pinned_oracle_isolates_the_backward_arithmetic(name):
     res = max(float((np.abs(g32[n]) / (U32 * absum[n])).max()) for n in ZERO_GRAD_BIAS)
     print(f"\n[{name}] float32 oracle zero-bias residue {res:.2f} x 2^-24 sum|gy|")
     # numpy's float32 run (pairwise sums, float32 InstanceNorm statistics): <= 11 on the
-    # well-conditioned fixtures, ~1.2e3 on the saturated-pattern one
-    assert res <= (4 * ZERO_BIAS_K if name == "vae128_b2_edge" else ZERO_BIAS_K)
+    # well-conditioned fixtures -- inside the GPU gate of every arithmetic -- and ~1.2e3 on the
+    # saturated-pattern one (its first InstanceNorm runs on a near-constant plane, rstd ~ 1e2;
+    # the GPU's own residue there is <= 3)
+    if name == "vae128_b2_edge":
+        assert res <= 2048
+    else:
+        assert res <= min(ZERO_BIAS_K.values())
 
 
 def test_reference_zero_bias_noise_record():
@@ -108,4 +113,4 @@ def test_reference_zero_bias_noise_record():
     ratios = [float((np.abs(z["db32/" + n]) / (U32 * z["absum/" + n])).max()) for n in z["names"]]
     f64 = [float((np.abs(z["db64/" + n]) / (U32 * z["absum/" + n])).max()) for n in z["names"]]
     print(f"\nreference fp32 residue at B=256: max {max(ratios):.3f} x 2^-24 sum|gy|; fp64 {max(f64):.1e}")
-    assert max(ratios) < 1.0 and max(f64) < 1e-6 and ZERO_BIAS_K >= 1.0
+    assert max(ratios) < 1.0 and max(f64) < 1e-6 and min(ZERO_BIAS_K.values()) >= 1.0
