@@ -26,6 +26,7 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus:
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -453,6 +454,11 @@ def main():
     plan = model.plan
 
     log(f"[bench] rank {rank}/{world} batch {args.batch} warmup {args.warmup} steps {args.steps}")
+    # EBSDVAE_CU_SPLIT=k (experiment): the step runs on the N - k CU stream,
+    # the weight gradients on the other k
+    split_main = E.cu_split_main(dev)
+    step_ctx = torch.cuda.stream(split_main) if split_main is not None else contextlib.nullcontext()
+    step_ctx.__enter__()
     for _ in range(args.warmup):
         trainer.step(x)
     torch.cuda.synchronize()
@@ -476,6 +482,7 @@ def main():
         else:
             out = trainer.step(x)
     torch.cuda.synchronize()
+    step_ctx.__exit__(None, None, None)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

@@ -3,6 +3,9 @@
 #include <stdio.h>
 
 #include <mutex>
+#include <vector>
+
+#include <hip/hip_ext.h>
 
 #include "common.h"
 #include "../../include/ebsdvae.h"
@@ -136,4 +139,72 @@ extern "C" int ebsdvae_fork_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signa
     return 2;
   }
   return 0;
+}
+
+// ------------------------------------------------------------------ CU-partitioned streams
+// A stream restricted to the CU-mask bits [first, first + count) (hipExtStreamCreateWithCUMask).
+// On MI355X the runtime spreads N contiguous mask bits evenly over the 8 XCDs (N / 8 CUs each;
+// tools/micro/cumask_probe.hip), so complementary ranges give two disjoint CU sets with the same
+// share of every XCD.  The count is registered for the stream: the persistent conv kernels
+// launched on it size their grids by it (one block per CU of the set).  Round-5 experiment of
+// the CU-partitioned backward: input-gradient chain on one set, weight
+// gradients on the other.
+namespace {
+constexpr int kMaxCuStreams = 16;
+hipStream_t g_cu_stream[kMaxCuStreams];
+int g_cu_count[kMaxCuStreams];
+std::mutex g_cu_mu;
+}  // namespace
+
+namespace evh {
+int stream_cus(hipStream_t s) {
+  if (!s) return 0;
+  std::lock_guard<std::mutex> lock(g_cu_mu);
+  for (int i = 0; i < kMaxCuStreams; ++i)
+    if (g_cu_stream[i] == s) return g_cu_count[i];
+  return 0;
+}
+}  // namespace evh
+
+extern "C" int ebsdvae_stream_create_cus(int first, int count, ebsdvae_stream_t* out) {
+  int ncu = 0, dev = 0;
+  EV_REQUIRE(out != nullptr, "stream_create_cus: null output");
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    evh::set_error("stream_create_cus: no device");
+    return 2;
+  }
+  EV_REQUIRE(first >= 0 && count > 0 && first + count <= ncu && count % 8 == 0,
+             "stream_create_cus: CUs [%d, %d) outside [0, %d) or not a multiple of 8", first,
+             first + count, ncu);
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int i = first; i < first + count; ++i) mask[i / 32] |= 1u << (i % 32);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+    evh::set_error("stream_create_cus: hipExtStreamCreateWithCUMask failed");
+    return 2;
+  }
+  std::lock_guard<std::mutex> lock(g_cu_mu);
+  for (int i = 0; i < kMaxCuStreams; ++i)
+    if (!g_cu_stream[i]) {
+      g_cu_stream[i] = s;
+      g_cu_count[i] = count;
+      *out = (ebsdvae_stream_t)s;
+      return 0;
+    }
+  (void)hipStreamDestroy(s);
+  evh::set_error("stream_create_cus: more than %d CU-masked streams", kMaxCuStreams);
+  return 2;
+}
+
+extern "C" int ebsdvae_stream_destroy_cus(ebsdvae_stream_t stream) {
+  std::lock_guard<std::mutex> lock(g_cu_mu);
+  for (int i = 0; i < kMaxCuStreams; ++i)
+    if (g_cu_stream[i] == (hipStream_t)stream) {
+      g_cu_stream[i] = nullptr;
+      g_cu_count[i] = 0;
+      return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? 0 : 2;
+    }
+  evh::set_error("stream_destroy_cus: not a stream of ebsdvae_stream_create_cus");
+  return 1;
 }

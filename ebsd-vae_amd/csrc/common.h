@@ -203,6 +203,9 @@ int check_launch(const char* what);
 // the event armed by ebsdvae_fork_arm for the next gy-producing launch (nullptr if none); the
 // caller attaches it to that launch (hipExtLaunchKernel stopEvent)
 hipEvent_t take_fork_event();
+// compute units a stream may run on: the count registered by ebsdvae_stream_create_cus for a
+// CU-masked stream, else 0 (the device's; the persistent kernels size their grids by it)
+int stream_cus(hipStream_t s);
 }  // namespace evh
 
 // a spatial extent the shape queries accept (H * W and its multiples stay inside int)

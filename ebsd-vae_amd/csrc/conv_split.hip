@@ -1293,8 +1293,10 @@ static bool use_wres() {
   return v;
 }
 
-// compute units of the current device (cached per device id)
-static int cu_count() {
+// compute units the persistent kernels launched on stream s own: the registered count of a
+// CU-masked stream (ebsdvae_stream_create_cus), else the current device's (cached per device id)
+static int cu_count(hipStream_t s) {
+  if (const int n = evh::stream_cus(s)) return n;
   static int cache[64] = {0};
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -1383,7 +1385,7 @@ static bool plan_split(int H, int W, int cin, int cout, int np, X3Cfg* c) {
 // InstanceNorm finalize of its own images after its last tile?  (B = 256 at 128^2: 32 tiles of
 // 4 rows per image, 8192 tiles over 256 CUs -> exactly one image per block.)
 // EBSDVAE_FUSE_FINALIZE=0 always takes the standalone finalize kernels (A/B, tests).
-static bool pipe_owns_images(const X3Cfg& c, int B, int H) {
+static bool pipe_owns_images(const X3Cfg& c, int B, int H, hipStream_t s) {
   static const bool on = [] {
     const char* e = getenv("EBSDVAE_FUSE_FINALIZE");
     return !(e && e[0] == '0');
@@ -1391,7 +1393,7 @@ static bool pipe_owns_images(const X3Cfg& c, int B, int H) {
   if (!on || !(c.NI > 1 || (use_pipe() && c.lds_pipe))) return false;
   const int tpi = c.NI > 1 ? 1 : H / c.TH;
   const int ntiles = ((B + c.NI - 1) / c.NI) * tpi;
-  const int ncu = cu_count();
+  const int ncu = cu_count(s);
   const int tpb = (ntiles + ncu - 1) / ncu;
   return tpb % tpi == 0;
 }
@@ -1409,7 +1411,7 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
       once = true;
     }
     // one block per CU, each owning a contiguous run of tiles
-    const int ncu = cu_count();
+    const int ncu = cu_count(s);
     const int tpb = (ntiles + ncu - 1) / ncu;
     const int nblk = (ntiles + tpb - 1) / tpb;
     hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), c.lds_pipe, s, src, (const float2*)st,
@@ -1668,7 +1670,7 @@ extern "C" int ebsdvae_conv3x3_fwd_split_st(const float* src, const float* src_s
   EV_REQUIRE(plan_split(H, W, cin, cout, pieces, &c),
              "conv3x3_fwd_split_st: unsupported shape H=%d W=%d cin=%d cout=%d pieces=%d", H, W, cin,
              cout, pieces);
-  const bool fused = pipe_owns_images(c, B, H);
+  const bool fused = pipe_owns_images(c, B, H, (hipStream_t)stream);
   InBwdFuse f;
   f.ypool = ypool;
   if (fused) f.st_out = (float2*)st;
@@ -1699,7 +1701,7 @@ extern "C" int ebsdvae_conv3x3_dgrad_inbwd_f16_bst(const float* g, const float* 
              "conv3x3_dgrad_inbwd_f16_bst: summed upsample adjoint unsupported for H=%d W=%d", H, W);
   EV_REQUIRE(plan_split(H, W, cin, cout, NP_F16, &c),
              "conv3x3_dgrad_inbwd_f16_bst: unsupported shape H=%d W=%d cin=%d cout=%d", H, W, cin, cout);
-  const bool fused = pipe_owns_images(c, B, H);
+  const bool fused = pipe_owns_images(c, B, H, (hipStream_t)stream);
   InBwdFuse f;
   f.yprev = y_prev;
   f.stprev = (const float2*)st_prev;

@@ -114,6 +114,23 @@ static int wg_pipe_cot(int cout) {
   }();
   return cout == 32 ? 32 : ((wide && cout % 128 == 0) ? 128 : 64);
 }
+// input channels per block of the pipelined kernel: 64 for co 64 blocks where cin % 64 == 0
+// (co 64 x ci 64, 8 waves: gy is read once per layer instead of twice; 64->64 @64 236 -> 221 us,
+// round 5), else 32.  A co 128 x ci 64 block (waves of co 64 x ci 16) needs 144 accumulator
+// VGPRs and spilled 132-208 B per lane: 2x slower (wgrad128 195 -> 400 us), not used.
+// EBSDVAE_WG_CI64=0: always 32 (A/B); =2 also the co 128 x ci 64 blocks (experiment)
+static int wg_pipe_ci64_mode() {
+  static const int v = [] {
+    const char* e = getenv("EBSDVAE_WG_CI64");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+static int wg_pipe_cit(int cin, int cout) {
+  const int m = wg_pipe_ci64_mode();
+  if (m <= 0 || cout == 32 || cin % 64) return 32;
+  return (m >= 2 || wg_pipe_cot(cout) == 64) ? 64 : 32;
+}
 static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
   if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0) return false;
   if (H % 8 || W % 8 || cin % 32 || !(cout == 32 || cout % 64 == 0)) return false;
@@ -124,10 +141,11 @@ static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
   g->ntx = W / 8; g->nty = H / 8;
   g->lTW = 3; g->ltpx = 6;
   g->tiles = (int)((long)B * g->ntx * g->nty);
-  const int cot = wg_pipe_cot(cout);
+  const int cot = wg_pipe_cot(cout), cit = wg_pipe_cit(cin, cout);
   const int co_t = cout == 32 ? 1 : cout / cot;
   // 8-wave blocks fill a CU alone: half the block target keeps one wave of blocks
-  const int want = wg_block_target(64) / (cot == 128 ? 2 : 1) / (co_t * (cin / 32));
+  const bool eight = cot == 128 || cit == 64;
+  const int want = wg_block_target(64) / (eight ? 2 : 1) / (co_t * (cin / cit));
   int tps = 4;
   while ((g->tiles + tps - 1) / tps > (want > 1 ? want : 1)) tps *= 2;
   g->tps = tps;
@@ -137,7 +155,7 @@ static bool wg_pipe_geom(int B, int H, int W, int cin, int cout, WgGeom* g) {
 
 // 1-D grid of wgrad_pipe_kernel: 8 x ceil(slices / 8) x (co tiles x ci tiles) blocks
 static dim3 wg_pipe_grid(const WgGeom& g, int cin, int cout) {
-  const int nm = (cout == 32 ? 1 : cout / wg_pipe_cot(cout)) * (cin / 32);
+  const int nm = (cout == 32 ? 1 : cout / wg_pipe_cot(cout)) * (cin / wg_pipe_cit(cin, cout));
   return dim3(8 * ((g.slices + 7) / 8) * nm);
 }
 
@@ -455,20 +473,23 @@ constexpr int WGS_ASB = 96;   // activation image row stride (32 ch x 2 B + 32 B
 // the first through LDS (KSPLIT 2), store the slice's partial dW tile [slice][tap][co][ci]
 // (16x16 C/D: col = ci = lane & 15, row = co) with the gradient scale undone, and the bias
 // partial from the per-thread gy sums (ci tile 0 only).  LDS is free on entry.
-template <int NWCO, int KSPLIT, bool F16>
-EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[2][9], const double (&bs)[4], char* wsm,
+// FCO = 16-co fragments per wave (co tile of a wave 16 FCO), NWCI = ci-waves of 16 channels
+// (block ci tile 16 NWCI); the defaults are the co 32 x ci 16 waves of 32-channel ci tiles.
+template <int NWCO, int KSPLIT, bool F16, int FCO = 2, int NWCI = 2>
+EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[FCO][9], const double (&bs)[4], char* wsm,
                                   float* __restrict__ wpart, float* __restrict__ bpart, int slice,
                                   int co0, int ci0, int Cin, int Cout, float gsc, bool do_bias) {
-  constexpr int CO_T = NWCO * 32;
+  constexpr int CO_T = NWCO * 16 * FCO;
   constexpr int QG = CO_T / 4;
-  constexpr int NTH = NWCO * 2 * KSPLIT * 64;   // threads per block
+  constexpr int NTH = NWCO * NWCI * KSPLIT * 64;   // threads per block
+  constexpr int NACC = FCO * 9 * 4;                // accumulator floats per lane
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
+  const int wco = wave % NWCO, wci = (wave / NWCO) % NWCI, wk = wave / (NWCI * NWCO);
   if (KSPLIT == 2) {
-    float* xs = reinterpret_cast<float*>(wsm) + (size_t)(wave - 2 * NWCO) * 72 * 64;
+    float* xs = reinterpret_cast<float*>(wsm) + (size_t)(wave - NWCI * NWCO) * NACC * 64;
     if (wk == 1) {
 #pragma unroll
-      for (int f = 0; f < 2; ++f)
+      for (int f = 0; f < FCO; ++f)
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
@@ -476,9 +497,9 @@ EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[2][9], const double (&bs)[4], cha
     }
     __syncthreads();
     if (wk == 0) {
-      xs = reinterpret_cast<float*>(wsm) + (size_t)wave * 72 * 64;
+      xs = reinterpret_cast<float*>(wsm) + (size_t)wave * NACC * 64;
 #pragma unroll
-      for (int f = 0; f < 2; ++f)
+      for (int f = 0; f < FCO; ++f)
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
@@ -489,12 +510,12 @@ EV_DEVINL void wgrad_split_finish(f32x4 (&acc)[2][9], const double (&bs)[4], cha
   const int ci = ci0 + wci * 16 + (lane & 15);
   if (wk == 0) {
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+    for (int f = 0; f < FCO; ++f)
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int co = co0 + wco * 32 + f * 16 + (lane >> 4) * 4 + r;
+          const int co = co0 + wco * 16 * FCO + f * 16 + (lane >> 4) * 4 + r;
           // the slice partials are read once, by the batched reduction: non-temporal
           __builtin_nontemporal_store(F16 ? acc[f][tap][r] * (1.f / gsc) : acc[f][tap][r],
                                       wpart + (((size_t)slice * 9 + tap) * Cout + co) * Cin + ci);
@@ -736,9 +757,13 @@ EV_DEVINL void static_for(F&& f) {
 // spends most of its time there: without its staging it runs 2.3-2.7x faster, without its
 // loads 1.3x (tools/micro_variants.sh, EV_WG_NOSTORE / EV_WG_NOLOAD).
 // NWCO = 4 (co 128 x ci 32, 8 waves, one block per CU by LDS): the activation halo of a tile
-// is staged once per 128 output channels instead of once per 64 (EBSDVAE_WG_CO128)
-template <int NP, int NWCO, int KSPLIT, int MODE>
-__global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgrad_pipe_kernel(
+// is staged once per 128 output channels instead of once per 64 (EBSDVAE_WG_CO128).
+// NWCI = 4 (ci tile 64; round 5): with FCO = 4 (waves of co 64 x ci 16, 144 accumulator
+// registers) a co 128 x ci 64 block stages 0.64x the values per MAC of co 128 x ci 32 and reads
+// each B fragment for twice the MFMAs; with FCO = 2 a co 64 x ci 64 block reads gy once per
+// layer instead of twice (EBSDVAE_WG_CI64=0: the ci 32 blocks, A/B)
+template <int NP, int NWCO, int KSPLIT, int MODE, int NWCI = 2, int FCO = 2>
+__global__ __launch_bounds__(NWCO * NWCI * KSPLIT * 64, NWCO * NWCI * KSPLIT >= 8 ? 1 : 2) void wgrad_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats,
     const float* __restrict__ gy, float* __restrict__ wpart, float* __restrict__ bpart, int B,
     int H, int W, int Cin, int Cout, WgGeom g, const float* __restrict__ gmax, int gmT) {
@@ -746,41 +771,46 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
   using T = WgTileP<TW, PT>;               // one image, 8x8 pixels, 10x10 halo
   constexpr int NPC = npc(NP);
   constexpr bool F16 = NP == NP_F16;
-  constexpr int CO_T = NWCO * 32;
+  constexpr int CO_T = NWCO * 16 * FCO;
+  constexpr int CI_T = NWCI * 16;
   constexpr int GSB = CO_T * 2 + 32;       // gy image row stride (bytes)
+  constexpr int ASB = CI_T * 2 + 32;       // activation image row stride: 96 / 160 B
   constexpr int QG = CO_T / 4;
-  constexpr int NTH = NWCO * 2 * KSPLIT * 64;   // threads per block
+  constexpr int QH = CI_T / 4;             // float4 channel groups of a halo pixel
+  constexpr int NTH = NWCO * NWCI * KSPLIT * 64;   // threads per block
   constexpr int KG = PT * CO_T / 4 / NTH;  // gy float4 items per thread per tile
-  constexpr int KH = (T::HALO * 8 + NTH - 1) / NTH;
+  constexpr int KH = (T::HALO * QH + NTH - 1) / NTH;
   constexpr int NIT = KG + KH;
   constexpr int KSTEPS = PT / 32;
   constexpr int NSLOT = (KSTEPS / KSPLIT) * 9;   // (k-step, tap) slots per wave and tile
   constexpr int GY_PIECE = PT * GSB;
-  constexpr int ACT_PIECE = T::HALO * WGS_ASB;
+  constexpr int ACT_PIECE = T::HALO * ASB;
   constexpr int BUF = NPC * (GY_PIECE + ACT_PIECE);
   constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_UP);
   constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
   static_assert(T::NI == 1 && T::HP == 10 && T::WP == 10, "8x8 tiles");
-  static_assert(NWCO * 2 * KSPLIT == 4 || (NWCO == 4 && KSPLIT == 1), "4 or 8 waves per block");
+  static_assert(NWCO * NWCI * KSPLIT == 4 || NWCO * NWCI * KSPLIT == 8, "4 or 8 waves per block");
+  static_assert((NWCI == 2 || NWCI == 4) && (FCO == 2 || FCO == 4), "wave / block tiles");
+  static_assert(NTH % QG == 0 && NTH % QH == 0, "item channel groups fixed per thread");
   static_assert(KSTEPS % KSPLIT == 0 && NIT <= NSLOT, "item slots");
   static_assert(MODE != ACT_NORM_POOL, "pool-fed layers use the materialised activation");
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wco = wave % NWCO, wci = (wave / NWCO) & 1, wk = wave / (2 * NWCO);
+  const int wco = wave % NWCO, wci = (wave / NWCO) % NWCI, wk = wave / (NWCI * NWCO);
   // XCD-aware block order (1-D grid, wg_pipe_grid): blocks L and L + 8 share an XCD, so the
   // nm = (co tiles) x (ci tiles) blocks of one slice take consecutive L / 8 on ONE XCD and
   // read the slice's gy and activation rows while they are in that XCD's L2
-  const int nco = Cout / CO_T, nm = nco * (Cin / 32);
+  const int nco = Cout / CO_T, nm = nco * (Cin / CI_T);
   const int xcd = blockIdx.x & 7, wq = blockIdx.x >> 3, m = wq % nm;
   const int slice = (wq / nm) * 8 + xcd;
   if (slice >= g.slices) return;   // grid padding (whole block, before any barrier)
-  const int co0 = (m % nco) * CO_T, ci0 = (m / nco) * 32;
+  const int co0 = (m % nco) * CO_T, ci0 = (m / nco) * CI_T;
   const int Hs = UPS ? H / 2 : H, Ws = UPS ? W / 2 : W;
-  const int qh = tid & 7, qg = tid % QG;
+  const int qh = tid % QH, qg = tid % QG;
 
-  f32x4 acc[2][9];
+  f32x4 acc[FCO][9];
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
+  for (int f = 0; f < FCO; ++f)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   double bs[4] = {0.0, 0.0, 0.0, 0.0};
@@ -807,10 +837,10 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
   const int srow = Ws * Cin * 4;   // bytes per source row
 #pragma unroll
   for (int k = 0; k < KH; ++k) {
-    const int pix = (tid + NTH * k) >> 3;
+    const int pix = (tid + NTH * k) / QH;
     hdr[k] = pix < T::HALO ? pix / T::WP - 1 : -(1 << 20);   // dead item: never in range
     hdc[k] = pix % T::WP - 1;
-    hlo[k] = pix * WGS_ASB + qh * 8;
+    hlo[k] = pix * ASB + qh * 8;
     // UPS: (y0 + dr) >> 1 == y0 / 2 + (dr >> 1) for even y0 (arithmetic shift = floor)
     hbo[k] = pix < T::HALO ? (UPS ? (hdr[k] >> 1) * srow + (hdc[k] >> 1) * Cin * 4
                                   : hdr[k] * srow + hdc[k] * Cin * 4) + (ci0 + qh * 4) * 4
@@ -896,7 +926,7 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
 
   // per-lane transposed-read geometry (wgrad_split_kernel)
   const int gq = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
-  const int acol = (wco * 32 + 4 * p4) * 2;
+  const int acol = (wco * 16 * FCO + 4 * p4) * 2;
   const int bcol = (wci * 16 + 4 * p4) * 2;
 
   if (t_beg < t_end) {
@@ -928,11 +958,11 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
       constexpr int si = decltype(si_c)::value;
       const int s = wk + si * KSPLIT;
       const int px0 = 32 * s + 4 * gq + q, px1 = px0 + 16;
-      bf16x8w a[NPC][2];
+      bf16x8w a[NPC][FCO];
 #pragma unroll
       for (int i = 0; i < NPC; ++i)
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
+        for (int f = 0; f < FCO; ++f)
           a[i][f] = tr_frag(gimg + i * GY_PIECE + px0 * GSB + acol + f * 32,
                             gimg + i * GY_PIECE + px1 * GSB + acol + f * 32);
       const int hp0 = (px0 / TW) * T::WP + px0 % TW, hp1 = (px1 / TW) * T::WP + px1 % TW;
@@ -942,10 +972,10 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
         bf16x8w b[NPC];
 #pragma unroll
         for (int i = 0; i < NPC; ++i)
-          b[i] = tr_frag(aimg + i * ACT_PIECE + (hp0 + toff) * WGS_ASB + bcol,
-                         aimg + i * ACT_PIECE + (hp1 + toff) * WGS_ASB + bcol);
+          b[i] = tr_frag(aimg + i * ACT_PIECE + (hp0 + toff) * ASB + bcol,
+                         aimg + i * ACT_PIECE + (hp1 + toff) * ASB + bcol);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
+        for (int f = 0; f < FCO; ++f) {
           f32x4 c = acc[f][tap];
 #ifdef EV_WGP_NOMFMA   // timing experiment only (wrong results)
           c[0] += (float)a[0][f][0] * (float)b[0][0] + (float)a[1][f][1] * (float)b[1][1];
@@ -973,8 +1003,8 @@ __global__ __launch_bounds__(NWCO * 2 * KSPLIT * 64, NWCO == 4 ? 1 : 2) void wgr
     }
     __syncthreads();
   }
-  wgrad_split_finish<NWCO, KSPLIT, F16>(acc, bs, wsm, wpart, bpart, slice, co0, ci0, Cin, Cout, gsc,
-                                        ci0 == 0);
+  wgrad_split_finish<NWCO, KSPLIT, F16, FCO, NWCI>(acc, bs, wsm, wpart, bpart, slice, co0, ci0, Cin,
+                                                   Cout, gsc, ci0 == 0);
 }
 
 // ------------------------------------------------------------------ cin == 1 (first conv)
@@ -1306,18 +1336,18 @@ static void launch_wgs(dim3 grid, hipStream_t s, const float* src, const float* 
     launch_wgs_tw<NP, NWCO, KSPLIT, MODE, 8, PT>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT);
 }
 
-template <int NP, int NWCO, int KSPLIT, int MODE>
+template <int NP, int NWCO, int KSPLIT, int MODE, int NWCI = 2, int FCO = 2>
 static void launch_wgp(dim3 grid, hipStream_t s, const float* src, const float* st, const float* gy,
                        float* wpart, float* bpart, int B, int H, int W, int cin, int cout,
                        const WgGeom& g, const float* gmax, int gmT) {
-  constexpr int CO_T = NWCO * 32;
-  constexpr int NTH = NWCO * 2 * KSPLIT * 64;
-  const size_t lds_img = 2 * (size_t)npc(NP) * ((size_t)64 * (CO_T * 2 + 32) + (size_t)100 * WGS_ASB);
-  const size_t lds_fold = KSPLIT == 2 ? (size_t)2 * 72 * 64 * 4 : 0;
+  constexpr int CO_T = NWCO * 16 * FCO, CI_T = NWCI * 16;
+  constexpr int NTH = NWCO * NWCI * KSPLIT * 64;
+  const size_t lds_img = 2 * (size_t)npc(NP) * ((size_t)64 * (CO_T * 2 + 32) + (size_t)100 * (CI_T * 2 + 32));
+  const size_t lds_fold = KSPLIT == 2 ? (size_t)NWCO * NWCI * FCO * 36 * 64 * 4 : 0;
   size_t lds = lds_img;
   if (lds < lds_fold) lds = lds_fold;
   if (lds < (size_t)NTH * 4 * 8) lds = (size_t)NTH * 4 * 8;
-  auto k = wgrad_pipe_kernel<NP, NWCO, KSPLIT, MODE>;
+  auto k = wgrad_pipe_kernel<NP, NWCO, KSPLIT, MODE, NWCI, FCO>;
   static bool once = false;
   if (!once) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1337,6 +1367,20 @@ static void dispatch_wgp(int mode, bool narrow, dim3 grid, hipStream_t s, const 
       case ACT_NORM: launch_wgp<NP, 1, 2, ACT_NORM>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
       case ACT_UP: launch_wgp<NP, 1, 2, ACT_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
       default: launch_wgp<NP, 1, 2, ACT_NORM_UP>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+    }
+  } else if (wg_pipe_cit(cin, cout) == 64 && wg_pipe_cot(cout) == 128) {   // co 128 x ci 64
+    switch (mode) {
+      case ACT_RAW: launch_wgp<NP, 2, 1, ACT_RAW, 4, 4>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_NORM: launch_wgp<NP, 2, 1, ACT_NORM, 4, 4>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_UP: launch_wgp<NP, 2, 1, ACT_UP, 4, 4>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      default: launch_wgp<NP, 2, 1, ACT_NORM_UP, 4, 4>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+    }
+  } else if (wg_pipe_cit(cin, cout) == 64) {   // co 64 x ci 64
+    switch (mode) {
+      case ACT_RAW: launch_wgp<NP, 2, 1, ACT_RAW, 4, 2>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_NORM: launch_wgp<NP, 2, 1, ACT_NORM, 4, 2>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      case ACT_UP: launch_wgp<NP, 2, 1, ACT_UP, 4, 2>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
+      default: launch_wgp<NP, 2, 1, ACT_NORM_UP, 4, 2>(grid, s, src, st, gy, wpart, bpart, B, H, W, cin, cout, g, gmax, gmT); break;
     }
   } else if (wg_pipe_cot(cout) == 128) {
     switch (mode) {

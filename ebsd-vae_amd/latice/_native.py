@@ -28,6 +28,8 @@ SIGNATURES = {
     "ebsdvae_stream_wait": [P, P],
     "ebsdvae_fork_arm": [P],
     "ebsdvae_fork_wait": [P, P],
+    "ebsdvae_stream_create_cus": [I, I, P],
+    "ebsdvae_stream_destroy_cus": [P],
     "ebsdvae_conv_first_stat_tiles": [I, I],
     "ebsdvae_conv_first_fwd": [P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_apply_wgrad_rc": [P, P, P, P, P, P, P, P, I, I, I, I, P],

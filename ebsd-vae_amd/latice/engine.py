@@ -587,11 +587,43 @@ def _dev_key(device):
     return device.index if device.index is not None else torch.cuda.current_device()
 
 
+# EBSDVAE_CU_SPLIT=k (experiment): the weight-gradient side stream runs on
+# k compute units (CU-mask bits [N - k, N), N / 8 of them on every XCD) and cu_split_main()
+# gives the complementary N - k for the input-gradient chain, whose persistent conv kernels then
+# launch N - k blocks (ebsdvae_stream_create_cus).  The caller runs the step on that stream.
+_CU_SPLIT = int(os.environ.get("EBSDVAE_CU_SPLIT", "0"))
+_CU_MAIN = {}
+
+
+def _cu_stream(device, first, count):
+    import ctypes as C
+    out = C.c_void_p()
+    with torch.cuda.device(device):
+        N.call("ebsdvae_stream_create_cus", first, count, C.byref(out))
+    return torch.cuda.ExternalStream(out.value, device=device)
+
+
+def cu_split_main(device):
+    """The CU-partitioned main stream of `device` under EBSDVAE_CU_SPLIT (None otherwise)."""
+    if _CU_SPLIT <= 0:
+        return None
+    key = _dev_key(device)
+    if key not in _CU_MAIN:
+        ncu = torch.cuda.get_device_properties(key).multi_processor_count
+        _CU_MAIN[key] = _cu_stream(torch.device("cuda", key), 0, ncu - _CU_SPLIT)
+    return _CU_MAIN[key]
+
+
 def side_stream(device):
-    """The weight-gradient side stream of `device` (created on first use)."""
+    """The weight-gradient side stream of `device` (created on first use; CU-masked to
+    EBSDVAE_CU_SPLIT compute units when set)."""
     key = _dev_key(device)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=device)
+        if _CU_SPLIT > 0:
+            ncu = torch.cuda.get_device_properties(key).multi_processor_count
+            _SIDE[key] = _cu_stream(torch.device("cuda", key), ncu - _CU_SPLIT, _CU_SPLIT)
+        else:
+            _SIDE[key] = torch.cuda.Stream(device=device)
     return _SIDE[key]
 
 

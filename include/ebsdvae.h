@@ -53,6 +53,12 @@ int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler);
  * Per host thread. */
 int ebsdvae_fork_arm(ebsdvae_stream_t signaler);
 int ebsdvae_fork_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler);
+/* CU-partitioned streams (experiment): a new stream restricted to the
+ * compute units of CU-mask bits [first, first + count) (count a multiple of 8; the runtime
+ * spreads contiguous bits evenly over the XCDs).  The persistent conv kernels launched on it
+ * size their grids by `count`.  Destroy with ebsdvae_stream_destroy_cus. */
+int ebsdvae_stream_create_cus(int first, int count, ebsdvae_stream_t* out);
+int ebsdvae_stream_destroy_cus(ebsdvae_stream_t stream);
 
 /* ---- weights ------------------------------------------------------------------------
  * Pack a Conv2d (kind 0: (cout,cin,3,3), latice/model.py:95,148) or ConvTranspose2d

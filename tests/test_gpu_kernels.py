@@ -781,7 +781,7 @@ def test_dgrad_summed_upsample_adjoint(cuda, cin, cout, H, prec):
 WG_F16_CASES = [  # (cin, cout, H, source mode, kind): NORM, NORM_UP and pooled-RAW sources
     (32, 32, 128, E.ACT_NORM, 0), (32, 64, 64, E.ACT_NORM_POOL, 0), (64, 128, 32, E.ACT_NORM_POOL, 0),
     (128, 64, 32, E.ACT_NORM, 1), (64, 32, 64, E.ACT_NORM, 1), (32, 32, 128, E.ACT_NORM_UP, 1),
-    (128, 128, 16, E.ACT_NORM_UP, 1), (64, 64, 64, E.ACT_NORM, 0),
+    (128, 128, 16, E.ACT_NORM_UP, 1), (64, 64, 64, E.ACT_NORM, 0), (128, 128, 32, E.ACT_NORM, 0),
 ]
 
 
