@@ -58,6 +58,9 @@ SIGNATURES = {
     "ebsdvae_conv3x3_wgrad_split_slices": [I, I, I, I, I, I],
     "ebsdvae_conv3x3_wgrad_split": [P, P, I, P, P, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_wgrad_f16": [P, P, I, P, P, I, P, P, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_dwgrad_slices": [I, I, I, I, I],
+    "ebsdvae_conv3x3_dwgrad_stat_tiles": [I, I],
+    "ebsdvae_conv3x3_dwgrad_f16": [P, P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, P],
     "ebsdvae_wgrad_reduce_work": [I, I, I],
     "ebsdvae_wgrad_reduce": [P, P, I, P, P, I, I, I, P, P],
     "ebsdvae_wgrad_reduce_batch_work": [P, I],
@@ -110,7 +113,8 @@ QUERIES = {"ebsdvae_version", "ebsdvae_conv_first_stat_tiles", "ebsdvae_conv3x3_
            "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_in_bwd_final_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work", "ebsdvae_heads_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
            "ebsdvae_conv3x3_split_pool_ok",
-           "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices", "ebsdvae_net_end_tiles"}
+           "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices", "ebsdvae_net_end_tiles",
+           "ebsdvae_conv3x3_dwgrad_slices", "ebsdvae_conv3x3_dwgrad_stat_tiles"}
 
 # include/ebsdvae.h EBSDVAE_ABI_VERSION: the signatures above
 ABI_VERSION = 2

@@ -1035,6 +1035,49 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False, ypool=
     return gin, part
 
 
+# ebsdvae_conv3x3_dwgrad_f16 (csrc/conv_fused.hip): the input gradient (with the previous
+# block's fused InstanceNorm-backward reduce) and the weight gradient of a 32 -> 32 layer in one
+# pass over gy and y_prev (encoder.1, decoder.13).  Opt-in (EBSDVAE_DWFUSE=1): measured in the
+# B = 256 step it is 0.17 ms slower than the separate kernels, whose weight gradient overlaps the
+# next input gradient on the side stream.
+_DWFUSE = os.environ.get("EBSDVAE_DWFUSE", "0") == "1"
+
+
+def dwgrad_ok(gy, layer: ConvLayer, wd, src_mode, prev_pmode) -> bool:
+    """The fused kernel covers `layer` (split-fp16 gy with maxima, 32 channels, a source that is
+    the normalised [upsampled] previous block and the matching reduce routing)."""
+    if wd is None or wd.pieces != PIECES_F16 or getattr(gy, "ev_gmax", None) is None:
+        return False
+    if (src_mode, prev_pmode) not in ((ACT_NORM, P_ID), (ACT_NORM_UP, P_UP)):
+        return False
+    B, H, W, _ = gy.shape
+    return N.call("ebsdvae_conv3x3_dwgrad_slices", B, H, W, layer.cin, layer.cout) > 0
+
+
+def conv_dwgrad(gy, layer: ConvLayer, wd, src, sst, src_mode, dw, db):
+    """Fused input + weight gradient (dwgrad_ok): returns (gin, part) like conv_dgrad(...,
+    prev=(src, sst, P_ID | P_UP), sum_up=True) -- gin is h at src's resolution -- and queues the
+    weight gradient's slice reduction like conv_wgrad."""
+    B, H, W, _ = gy.shape
+    gmax = gy.ev_gmax
+    S_ = N.call("ebsdvae_conv3x3_dwgrad_slices", B, H, W, layer.cin, layer.cout)
+    T = N.call("ebsdvae_conv3x3_dwgrad_stat_tiles", H, W)
+    Hs, Ws = src.shape[1], src.shape[2]
+    gin = _empty(B, Hs, Ws, layer.cin, like=gy)
+    part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
+    wpart = _empty(S_, 9, layer.cout, layer.cin, like=gy)
+    bpart = _empty(S_, layer.cout, like=gy)
+    tag = f"dwgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d} m{src_mode}"
+    flops = 2 * conv_flops(B, H, W, layer.cin, layer.cout)
+    nb = 4 * (gy.numel() + src.numel() + gin.numel())   # algorithmic I/O: gy, y_prev in, h out
+    _launch("conv3x3_dwgrad", flops, N.call, "ebsdvae_conv3x3_dwgrad_f16", N.ptr(gy), N.ptr(gmax),
+            gmax.shape[1], N.ptr(wd.t), N.ptr(src), N.ptr(sst), src_mode, N.ptr(gin),
+            part.data_ptr(), N.ptr(wpart), N.ptr(bpart), B, H, W, layer.cin, layer.cout, N.stream(),
+            tag=tag, pieces=wd.pieces, nbytes=nb)
+    _reduce_slices(wpart, bpart, S_, layer.cin, layer.cout, layer.kind, dw, db)
+    return gin, part
+
+
 def _grad_buf(grads, name, like):
     if grads is not None and name in grads:
         return grads[name]
@@ -1116,8 +1159,19 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
             in_backward_first(g_next, y, st, x, dw, db, part=part, w0=params[wn], b0=params[bn])
             out[wn], out[bn] = dw, db
             break
-        fk = fork_arm(y.device)   # the weight gradient below forks on the apply's completion
+        P = plan.enc[i - 1] if i > 0 else None
+        fused = (P is not None and L.src_mode == ACT_NORM and L.name + ".pool_in" not in saved
+                 and _DWFUSE and _FWD_PIECES.get(_PRECISION) and L.cin == 32 and L.cout == 32)
+        fk = False if fused else fork_arm(y.device)   # the weight gradient forks on the apply
         gy = in_backward(g_next, L.pmode, y, st, part=part)
+        wn, bn = L.name + ".weight", L.name + ".bias"
+        if fused and dwgrad_ok(gy, L, _wp(packs, L.name, 1), ACT_NORM, P.pmode):
+            dw = _grad_buf(grads, wn, params[wn])
+            db = _grad_buf(grads, bn, params[bn])
+            y_p, st_p = saved[P.name]
+            g_next, part = conv_dwgrad(gy, L, _wp(packs, L.name, 1), y_p, st_p, ACT_NORM, dw, db)
+            out[wn], out[bn] = dw, db
+            continue
         mode = L.src_mode
         if i == 0:
             src, sst = x, None
@@ -1127,7 +1181,6 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
             src, sst, mode = saved[L.name + ".act_in"], None, ACT_RAW
         else:
             src, sst = saved[plan.enc[i - 1].name]
-        wn, bn = L.name + ".weight", L.name + ".bias"
         dw = _grad_buf(grads, wn, params[wn])
         db = _grad_buf(grads, bn, params[bn])
         # every source but the raw input image is a normalised activation (.act_in included)
@@ -1279,6 +1332,12 @@ def _decoder_backward(plan, g_xhat, saved, params, grads, packs, end=None):
         src, sst = (saved["__dec_in__"], None) if i == 0 else saved[plan.dec[i - 1].name]
         dw = _grad_buf(grads, wn, params[wn])
         db = _grad_buf(grads, bn, params[bn])
+        if _DWFUSE and i > 0 and L.src_mode in (ACT_NORM, ACT_NORM_UP) and \
+                dwgrad_ok(gy, L, _wp(packs, L.name, 1), L.src_mode, plan.dec[i - 1].pmode):
+            # input + weight gradient in one pass (the last block's gy has no side-stream fork)
+            g_next, part = conv_dwgrad(gy, L, _wp(packs, L.name, 1), src, sst, L.src_mode, dw, db)
+            out[wn], out[bn] = dw, db
+            continue
         conv_wgrad(src, sst, L.src_mode, gy, L.cin, L.cout, L.kind, dw, db, fork=fk)
         out[wn], out[bn] = dw, db
         if i > 0:

@@ -242,6 +242,22 @@ int ebsdvae_conv3x3_wgrad_f16(const float* src, const float* src_stats, int src_
                               const float* gy, const float* gmax, int gm_tiles, float* wpart,
                               float* bpart, int B, int H, int W, int cin, int cout,
                               ebsdvae_stream_t stream);
+/* Fused input + weight gradient of a 32 -> 32 layer whose source is the previous block's
+ * normalised output (src_mode ACT_NORM: y_prev at H x W, its InstanceNorm-backward reduce routed
+ * P_ID; ACT_NORM_UP: y_prev at H/2 x W/2, the input gradient 2x2-summed, P_UPSUM) in one pass
+ * over gy and y_prev (encoder.1 / decoder.13 of latice/model.py:95-106): what
+ * ebsdvae_conv3x3_dgrad_inbwd_f16(..., pmode) and ebsdvae_conv3x3_wgrad_f16 compute together.
+ * wpack: the layer's split-fp16 input-gradient pack; gin (h = g * lrelu'(xhat_prev)) at
+ * y_prev's resolution; part (B, T, 32) double2 with T = ebsdvae_conv3x3_dwgrad_stat_tiles(H, W)
+ * (finalize over y_prev's H*W with ebsdvae_in_bwd_finalize); wpart / bpart
+ * ebsdvae_conv3x3_dwgrad_slices(...) slice partials for ebsdvae_wgrad_reduce(_batch).
+ * H == W, H / 8 a power of two. */
+int ebsdvae_conv3x3_dwgrad_slices(int B, int H, int W, int cin, int cout);
+int ebsdvae_conv3x3_dwgrad_stat_tiles(int H, int W);
+int ebsdvae_conv3x3_dwgrad_f16(const float* gy, const float* gmax, int gm_tiles, const void* wpack,
+                               const float* y_prev, const float* st_prev, int src_mode, float* gin,
+                               double* part, float* wpart, float* bpart, int B, int H, int W,
+                               int cin, int cout, ebsdvae_stream_t stream);
 int ebsdvae_wgrad_reduce(const float* wpart, const float* bpart, int slices, float* dw,
                          float* db, int cin, int cout, int kind, void* work,
                          ebsdvae_stream_t stream);

@@ -82,12 +82,14 @@ def test_graph_side_switch_gives_bitwise_equal_steps(cuda, monkeypatch):
 
 @pytest.mark.parametrize("switch", ["attr:_FIRST_VALU", "attr:_NET_END", "env:EBSDVAE_POOL_OUT",
                                     "env:EBSDVAE_WGRAD_F16", "env:EBSDVAE_POOL_REDUCE",
-                                    "env:EBSDVAE_UPSUM"])
+                                    "env:EBSDVAE_UPSUM", "on:_DWFUSE"])
 @pytest.mark.parametrize("prec", ["f16x3", "bf16x6"])
 def test_arithmetic_switch_meets_pinned_gates(cuda, monkeypatch, switch, prec):
     kind, name = switch.split(":")
     if kind == "attr":
         monkeypatch.setattr(E, name, False)
+    elif kind == "on":   # an opt-in path (EBSDVAE_DWFUSE=1: the fused input + weight gradient)
+        monkeypatch.setattr(E, name, True)
     else:
         monkeypatch.setenv(name, "0")
     f, m = _model(cuda)

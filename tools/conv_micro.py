@@ -52,6 +52,10 @@ CASES = {
     "wgrad128": ("wgrad", 32, 128, 128, ACT_NORM),
     "wgrad128s16": ("wgrad", 16, 128, 128, ACT_NORM),
     "wgrad64to128": ("wgrad", 32, 64, 128, ACT_NORM),
+    # fused input + weight gradient of the 32-channel layers (csrc/conv_fused.hip): encoder.1
+    # (same-resolution source, P_ID reduce) and decoder.13 (upsampled source, summed adjoint)
+    "dwgrad32": ("dwgrad", 128, 32, 32, ACT_NORM),
+    "dwgrad32u": ("dwgrad", 128, 32, 32, ACT_NORM_UP),
 }
 
 
@@ -108,6 +112,27 @@ def run(name, reps, pieces, B, warm=1.0):
                 return
             N.call("ebsdvae_conv3x3_dgrad_inbwd_split", gy.data_ptr(), wp.data_ptr(), gin.data_ptr(),
                    yprev.data_ptr(), stp.data_ptr(), mode, part.data_ptr(), B, H, H, cout, cin, pieces, s)
+    elif kind == "dwgrad":
+        flops *= 2   # both contractions
+        Hs = H // 2 if mode == ACT_NORM_UP else H
+        src = torch.randn(B, Hs, Hs, cin, device=dev, generator=g)
+        st = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
+        gy = torch.randn(B, H, H, cout, device=dev, generator=g)
+        wp = torch.empty(N.call("ebsdvae_pack_split_bytes", cout, cin, 16) // 4, device=dev)
+        d = (N.PackDesc * 1)(N.PackDesc(w.data_ptr(), wp.data_ptr(), cin, cout, 0, 1))
+        N.call("ebsdvae_pack_conv_weights_split", ctypes.addressof(d), 1, 16, s)
+        S_ = N.call("ebsdvae_conv3x3_dwgrad_slices", B, H, H, cin, cout)
+        T = N.call("ebsdvae_conv3x3_dwgrad_stat_tiles", H, H)
+        wpart = torch.empty(S_, 9, cout, cin, device=dev)
+        bpart = torch.empty(S_, cout, device=dev)
+        gin = torch.empty(B, Hs, Hs, cin, device=dev)
+        part = torch.empty(B, T, cin, 2, dtype=torch.float64, device=dev)
+        gmx = gy.abs().reshape(B, 4, -1).amax(2).contiguous()
+
+        def launch():
+            N.call("ebsdvae_conv3x3_dwgrad_f16", gy.data_ptr(), gmx.data_ptr(), 4, wp.data_ptr(),
+                   src.data_ptr(), st.data_ptr(), mode, gin.data_ptr(), part.data_ptr(),
+                   wpart.data_ptr(), bpart.data_ptr(), B, H, H, cin, cout, s)
     else:
         Hs = H // 2 if mode == ACT_NORM_UP else H
         src = torch.randn(B, Hs, Hs, cin, device=dev, generator=g)
