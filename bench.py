@@ -204,6 +204,15 @@ def encoder_latents(model, plan, args, dev, world):
             mu = E.encode_latents(plan, ingest_patterns(raw, (S, S), out=x), params, packs)
         torch.cuda.synchronize()
         eng = time.perf_counter() - t1
+        # attainable time of one batch: the encoder's conv launches from one
+        # event-bracketed encode (max(F/P, B/BW) each) + the transform's HBM bytes (read the
+        # float64 raw batch, write the fp32 crop)
+        with E.probe() as probe:
+            E.encode_latents(plan, ingest_patterns(raw, (S, S), out=x), params, packs)
+        torch.cuda.synchronize()
+        conv_att = probe.attainable_s(HBM_PEAK_GBS * 1e9)
+        ingest_att = (8.0 * B * H0 * H0 + 4.0 * B * S * S) / (HBM_PEAK_GBS * 1e9)
+        heads_att = (4.0 * B * plan.feat + 4.0 * 2 * plan.feat * plan.latent_dim) / (HBM_PEAK_GBS * 1e9)
         # query leg: 4096 perturbed latents, top-20 + consensus over the whole dictionary
         q = (mu.repeat(4, 1) + 0.01 * torch.randn(4 * B, plan.latent_dim, device=dev, generator=gen))
         db.find_best_orientations_batch(q[:64], top_n=20)   # warm-up
@@ -224,6 +233,14 @@ def encoder_latents(model, plan, args, dev, world):
             "value": round(n / el, 1), "unit": "latents/s", "latents": n,
             "ms_per_batch": round(el / nb * 1e3, 3),
             "tflops": round(enc_flops * n / el / 1e12, 2), "finite": finite,
+            "roofline": {"definition": "sum_k max(F_k/P_k, B_k/BW) per batch / measured ms per batch "
+                                       "(SURVEY.md 8d): encoder conv launches (event-probed) + "
+                                       "transform + heads bytes",
+                         "attainable_ms_per_batch": round((conv_att + ingest_att + heads_att) * 1e3, 3),
+                         "conv_attainable_ms": round(conv_att * 1e3, 3),
+                         "measured_ms_per_batch": round(el / nb * 1e3, 3),
+                         "frac": round((conv_att + ingest_att + heads_att) / (el / nb), 4),
+                         "engine_only_frac": round((conv_att + ingest_att + heads_att) / (eng / ne), 4)},
             "engine_only": {"value": round(world * B * ne / eng, 1), "unit": "latents/s",
                             "batches": ne, "what": "transform + encode_latents, no host copy"},
             "query": {"metric": "queries/sec (cosine top-20 over the dictionary + orientation "
@@ -263,13 +280,22 @@ def c5_step_rate(args, dev, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     loss = float(out[0])
+    ms = el / args.c5_steps * 1e3
     step_tflops = step_flops_per_pattern(model.plan) * B * args.c5_steps / el / 1e12
+    # the attainable step from one extra event-bracketed step after the timed
+    # ones (serial streams, so every launch is timed alone), against the timed step time
+    from latice import engine as E
+    with E.probe() as probe, E.serial_streams():
+        trainer.step(x)
+    torch.cuda.synchronize()
+    roof = step_roofline(probe, model.plan, B, ms, 1, trainer.numel)
     del trainer, model, x
     torch.cuda.empty_cache()
     return {"metric": "EBSD patterns/sec (256x256, latent 64, fwd+bwd)",
             "value": round(world * B * args.c5_steps / el, 2), "unit": "patterns/s",
             "batch_per_gpu": B, "global_batch": world * B, "steps": args.c5_steps,
-            "ms_per_step": round(el / args.c5_steps * 1e3, 3),
+            "ms_per_step": round(ms, 3),
+            "roofline": {"step": roof},
             "step_fp32_tflops": round(step_tflops, 2), "loss_finite": bool(np.isfinite(loss))}
 
 

@@ -1137,15 +1137,34 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True, packs_ready=N
     return out, saved
 
 
-def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=False, packs=None):
+def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=False, packs=None,
+                     after_wgrad=None):
     """g_enc: grad of the encoder output (B,s,s,C) NHWC.  Returns (grads dict, gx or None).
-    The layers' weight-gradient reductions run batched when it returns."""
+    The layers' weight-gradient reductions run batched when it returns.  after_wgrad:
+    {layer name: callable}: once that layer's weight gradient is issued, the reductions queued
+    so far are flushed (on the stream the weight gradients run on) and the callable runs -- the
+    trainer starts the all-reduce of the gradients finished by then (trainer.py)."""
     with batched_wgrad_reduce():
-        return _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs)
+        return _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs,
+                                 after_wgrad or {})
 
 
-def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
+def _flush_queued_reduces():
+    """Issue the weight-gradient reductions queued in the current batched_wgrad_reduce block."""
+    if _RQ:
+        q = list(_RQ)
+        _RQ.clear()
+        _flush_reduces(q)
+
+
+def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs, after_wgrad):
     out = {}
+
+    def done(name):
+        if name in after_wgrad:
+            _flush_queued_reduces()
+            after_wgrad[name]()
+
     g_next, part = g_enc, None
     gx = None
     for i in reversed(range(len(plan.enc))):
@@ -1158,6 +1177,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
             db = _grad_buf(grads, bn, params[bn])
             in_backward_first(g_next, y, st, x, dw, db, part=part, w0=params[wn], b0=params[bn])
             out[wn], out[bn] = dw, db
+            done(L.name)
             break
         P = plan.enc[i - 1] if i > 0 else None
         fused = (P is not None and L.src_mode == ACT_NORM and L.name + ".pool_in" not in saved
@@ -1171,6 +1191,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
             y_p, st_p = saved[P.name]
             g_next, part = conv_dwgrad(gy, L, _wp(packs, L.name, 1), y_p, st_p, ACT_NORM, dw, db)
             out[wn], out[bn] = dw, db
+            done(L.name)
             continue
         mode = L.src_mode
         if i == 0:
@@ -1186,6 +1207,7 @@ def _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs):
         # every source but the raw input image is a normalised activation (.act_in included)
         conv_wgrad(src, sst, mode, gy, L.cin, L.cout, L.kind, dw, db, normalized=i > 0, fork=fk)
         out[wn], out[bn] = dw, db
+        done(L.name)
         if i > 0:
             P = plan.enc[i - 1]
             g_next, part = conv_dgrad(gy, L, params[wn], prev=(*saved[P.name], P.pmode),

@@ -9,9 +9,12 @@ data-parallel version of it that the reference only gets implicitly from Lightni
   launch and the gradient exchange is two contiguous RCCL all-reduces.
 * Data parallelism (one process per GPU, torch.distributed "nccl" == RCCL over xGMI):
   every rank processes its own batch shard; the loss gradient is pre-scaled by 1/W so a
-  SUM all-reduce yields the mean gradient with no extra pass.  Bucket 0 (decoder + heads,
-  complete after the decoder backward) is all-reduced asynchronously while the encoder
-  backward runs; bucket 1 follows.  7.4 MB per step in total (1.85M fp32 parameters).
+  SUM all-reduce yields the mean gradient with no extra pass.  Three buckets, in the order
+  the backward completes them: 0 = decoder + heads (3.6 MB at 128x128, started after the
+  heads backward), 1 = the deep encoder layers at <= S/4 resolution (3.2 MB, started once
+  their weight gradients are issued, beside the shallow encoder backward), 2 = the shallow
+  encoder layers (0.26 MB, the only all-reduce left after the backward).  7.4 MB per step in
+  total (1.85M fp32 parameters); DESIGN.md section 6 gives the expected exposed time.
 * N == 1: the whole step can be captured into a hipGraph (capture()/replay()).
 """
 from __future__ import annotations
@@ -25,12 +28,17 @@ from .functional import dec_param_names, enc_param_names
 
 
 class GradReducer:
-    """Two-bucket asynchronous SUM all-reduce of a flat gradient buffer."""
+    """Bucketed asynchronous SUM all-reduce of a flat gradient buffer: `split` is one bucket
+    boundary (two buckets) or an increasing sequence of them."""
 
-    def __init__(self, gflat: torch.Tensor, split: int, group=None, force: bool = False):
+    def __init__(self, gflat: torch.Tensor, split, group=None, force: bool = False):
         """force: issue the all-reduces even in a group of one rank (tests run the collective
         path -- side-stream issue, wait ordering -- on a single GPU)."""
-        self.gflat, self.split, self.group = gflat, split, group
+        cuts = [int(split)] if isinstance(split, int) else [int(c) for c in split]
+        self.bounds = [0] + cuts + [gflat.numel()]
+        if any(b > c for b, c in zip(self.bounds, self.bounds[1:])):
+            raise ValueError(f"bucket boundaries must increase within the buffer: {self.bounds}")
+        self.gflat, self.split, self.group = gflat, cuts[0], group
         inited = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if inited else 1
         if force and not inited:
@@ -41,7 +49,9 @@ class GradReducer:
     def start(self, bucket: int):
         if not self.active:
             return
-        t = self.gflat[: self.split] if bucket == 0 else self.gflat[self.split:]
+        t = self.gflat[self.bounds[bucket]:self.bounds[bucket + 1]]
+        if t.numel() == 0:
+            return
         self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def finish(self):
@@ -74,7 +84,16 @@ class VAETrainer:
         if dev.type != "cuda":
             raise RuntimeError("VAETrainer needs the model on a ROCm device (no CPU fallback)")
         dec = dec_param_names(self.plan) + list(E.HEAD_NAMES)
-        enc = enc_param_names(self.plan)
+        # encoder parameters in the order the backward finishes them: the deep layers (at most
+        # S/4 resolution, 93 % of the encoder's parameters) first, then the shallow ones
+        S = self.plan.image_size
+        deep = [L for L in reversed(self.plan.enc) if L.H <= S // 4]
+        shallow = [L for L in reversed(self.plan.enc) if L.H > S // 4]
+        enc = [L.name + s for L in deep + shallow for s in (".weight", ".bias")]
+        if sorted(enc) != sorted(enc_param_names(self.plan)):
+            raise RuntimeError("unexpected encoder parameter set")
+        # the all-reduce of bucket 1 starts once the last deep layer's weight gradient is issued
+        self._deep_last = deep[-1].name if deep and shallow else None
         order = dec + enc
         if set(order) != set(params):
             raise RuntimeError("unexpected parameter set")
@@ -94,13 +113,15 @@ class VAETrainer:
                 self.G[n] = self.gflat[off:off + k].view_as(p)
                 off += k
         self.split = sum(params[n].numel() for n in dec)
+        n_deep = sum(params[L.name + s].numel() for L in deep for s in (".weight", ".bias"))
+        self.buckets = [self.split, self.split + n_deep] if self._deep_last else [self.split]
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
         self.max_exp_avg_sq = torch.zeros_like(self.flat) if self.amsgrad else None
         self.step_count = torch.zeros((), device=dev, dtype=torch.float32)
         self.one = torch.ones((), device=dev, dtype=torch.float32)
         self.noise_counter = torch.zeros(1, device=dev, dtype=torch.int64)
-        self.reducer = GradReducer(self.gflat, self.split, group, force=force_allreduce)
+        self.reducer = GradReducer(self.gflat, self.buckets, group, force=force_allreduce)
         self.world = self.reducer.world
         if self.world > 1:
             # every rank starts from rank 0's parameters (broadcast once
@@ -166,17 +187,29 @@ class VAETrainer:
                 _, g_dec = E.decoder_backward(plan, g_xhat, sd, P, grads=G, packs=packs)
             g_enc, _ = E.heads_backward(plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, P,
                                         grads=G)
+            hooks = {}
             if self.reducer.active:
                 # bucket 0 (decoder + heads) is complete on the side stream once it has
                 # caught up with the heads backward: the all-reduce is ordered behind it
-                side = E.side_stream(x.device)
-                E.stream_wait(side, torch.cuda.current_stream(x.device))
-                with torch.cuda.stream(side):
-                    self.reducer.start(0)
-            E.encoder_backward(plan, g_enc, x, se, P, grads=G, packs=packs)
-        self.reducer.start(1)
+                self._start_behind_side(0, x.device)
+                if self._deep_last:
+                    hooks[self._deep_last] = lambda: self._start_behind_side(1, x.device)
+            E.encoder_backward(plan, g_enc, x, se, P, grads=G, packs=packs, after_wgrad=hooks)
+        self.reducer.start(len(self.reducer.bounds) - 2)   # the last bucket
         self.reducer.finish()
         return loss, kl, rec
+
+    def _start_behind_side(self, bucket: int, device):
+        """Start a bucket's all-reduce behind everything issued so far on both streams: the
+        side stream carries the weight gradients (and their reductions), the current stream
+        the rest (heads backward, first-layer fused weight gradient)."""
+        if not E.side_streams_enabled():
+            self.reducer.start(bucket)
+            return
+        side = E.side_stream(device)
+        E.stream_wait(side, torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            self.reducer.start(bucket)
 
     def optimizer_step(self):
         b1, b2 = self.betas

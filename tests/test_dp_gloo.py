@@ -44,8 +44,18 @@ def _reducer_worker(rank, world, port, q):
     r.start(0)
     r.start(1)
     r.finish()
+    # three buckets (the trainer's decoder+heads / deep encoder / shallow encoder split),
+    # started out of order like the hooks can; an empty bucket is skipped
+    g3 = torch.arange(13, dtype=torch.float32) * (rank + 1)
+    r3 = GradReducer(g3, split=[3, 9, 9])
+    r3.start(1)
+    r3.start(0)
+    r3.start(2)
+    r3.start(3)
+    r3.finish()
     x = torch.arange(8).reshape(8, 1)
-    q.put((rank, g.numpy().copy(), shard_batch(x, rank, world).numpy().ravel().tolist()))
+    q.put((rank, g.numpy().copy(), shard_batch(x, rank, world).numpy().ravel().tolist(),
+           g3.numpy().copy()))
     dist.destroy_process_group()
 
 
@@ -87,9 +97,18 @@ def _run(fn, world=2):
 def test_grad_reducer_two_buckets_sum():
     out = _run(_reducer_worker)
     expect = np.arange(11, dtype=np.float32) * 3
-    for rank, g, shard in out:
+    for rank, g, shard, g3 in out:
         assert np.array_equal(g, expect)
         assert shard == list(range(4 * rank, 4 * rank + 4))
+        assert np.array_equal(g3, np.arange(13, dtype=np.float32) * 3)
+
+
+def test_grad_reducer_rejects_bad_boundaries():
+    from latice.trainer import GradReducer
+    with pytest.raises(ValueError, match="increase"):
+        GradReducer(torch.zeros(10), split=[6, 3])
+    with pytest.raises(ValueError, match="increase"):
+        GradReducer(torch.zeros(10), split=[12])
 
 
 @pytest.mark.timeout(600)
