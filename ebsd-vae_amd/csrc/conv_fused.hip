@@ -136,7 +136,10 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
   bool live[DW_K], inner[DW_K];
 #pragma unroll
   for (int k = 0; k < DW_K; ++k) {
-    const int hp = (tid + DW_NTH * k) >> 3;
+    // pixel ranks with bits 0 / 1 swapped: each 16-lane group of a ds_write_b64 stores pixels
+    // p, p + 2 (conflict-free, conv_wgrad.hip wg_store_perm)
+    int hp = (tid + DW_NTH * k) >> 3;
+    hp = (hp & ~3) | ((hp >> 1) & 1) | ((hp & 1) << 1);
     live[k] = hp < DW_HALO;
     const int hr = hp / DW_HP - 1, hc = hp % DW_HP - 1;
     hrc[k] = live[k] ? ((hr + 1) << 8) | (hc + 1) : 0;   // packed (row + 1, col + 1)

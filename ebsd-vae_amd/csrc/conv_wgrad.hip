@@ -762,6 +762,17 @@ EV_DEVINL void static_for(F&& f) {
 // registers) a co 128 x ci 64 block stages 0.64x the values per MAC of co 128 x ci 32 and reads
 // each B fragment for twice the MFMAs; with FCO = 2 a co 64 x ci 64 block reads gy once per
 // layer instead of twice (EBSDVAE_WG_CI64=0: the ci 32 blocks, A/B)
+// Staging-store order of the 8-B piece stores (ds_write_b64: 4 groups of 16 contiguous lanes,
+// banks (a/4) mod 32).  With 8 float4 items per pixel (32-channel images, 96-B rows) a group
+// stores two pixels, and consecutive pixels (rows 24 dwords apart) overlap in 8 banks: 2-way on
+// every store.  Swapping bits 0 and 1 of the pixel rank gives each group the pixels p, p + 2
+// (48 dwords apart = 16 mod 32): conflict-free.  Wider images store one pixel per group.
+template <int Q>
+EV_DEVINL int wg_store_perm(int r) {
+  if constexpr (Q == 8) return (r & ~3) | ((r >> 1) & 1) | ((r & 1) << 1);
+  return r;
+}
+
 template <int NP, int NWCO, int KSPLIT, int MODE, int NWCI = 2, int FCO = 2>
 __global__ __launch_bounds__(NWCO * NWCI * KSPLIT * 64, NWCO * NWCI * KSPLIT >= 8 ? 1 : 2) void wgrad_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats,
@@ -828,7 +839,7 @@ __global__ __launch_bounds__(NWCO * NWCI * KSPLIT * 64, NWCO * NWCI * KSPLIT >= 
   int gyo[KG], glo[KG];
 #pragma unroll
   for (int k = 0; k < KG; ++k) {
-    const int px = (tid + NTH * k) / QG, r = px / TW, c = px % TW;
+    const int px = wg_store_perm<QG>((tid + NTH * k) / QG), r = px / TW, c = px % TW;
     gyo[k] = (r * W + c) * Cout + co0 + qg * 4;
     glo[k] = px * GSB + qg * 8;
   }
@@ -837,7 +848,7 @@ __global__ __launch_bounds__(NWCO * NWCI * KSPLIT * 64, NWCO * NWCI * KSPLIT >= 
   const int srow = Ws * Cin * 4;   // bytes per source row
 #pragma unroll
   for (int k = 0; k < KH; ++k) {
-    const int pix = (tid + NTH * k) / QH;
+    const int pix = wg_store_perm<QH>((tid + NTH * k) / QH);
     hdr[k] = pix < T::HALO ? pix / T::WP - 1 : -(1 << 20);   // dead item: never in range
     hdc[k] = pix % T::WP - 1;
     hlo[k] = pix * ASB + qh * 8;
