@@ -799,6 +799,11 @@ __global__ __launch_bounds__(NWCO * NWCI * KSPLIT * 64, NWCO * NWCI * KSPLIT >= 
   constexpr int BUF = NPC * (GY_PIECE + ACT_PIECE);
   constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_UP);
   constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
+  // gy is read once per (co tile, slice): non-temporal loads for co <= 64 blocks, so the L2 keeps
+  // the activation halo rows neighbouring tiles re-read (64->64 @64 220 -> 208 us, 32->32 @128
+  // upsampled 265 -> 258 us; step within noise).  co 128 blocks measured
+  // slower with it (round 4).
+  constexpr int kGyPol = CO_T <= 64 ? 2 : 0;
   static_assert(T::NI == 1 && T::HP == 10 && T::WP == 10, "8x8 tiles");
   static_assert(NWCO * NWCI * KSPLIT == 4 || NWCO * NWCI * KSPLIT == 8, "4 or 8 waves per block");
   static_assert((NWCI == 2 || NWCI == 4) && (FCO == 2 || FCO == 4), "wave / block tiles");
@@ -897,7 +902,7 @@ __global__ __launch_bounds__(NWCO * NWCI * KSPLIT * 64, NWCO * NWCI * KSPLIT >= 
     constexpr int j = decltype(j_c)::value;
     if constexpr (j < KG) {
       rg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rgy, gtoff + gyo[j] * 4, 0, 0));
+                                             rgy, gtoff + gyo[j] * 4, 0, kGyPol));
     } else {
       // unconditional (the staging zeroes what lies outside the image): with every load
       // issued, the compiler's vmcnt waits count exactly one tile's loads
