@@ -23,15 +23,16 @@
 // Tiles are 8 x 8 pixels of one image; a block owns a slice (a contiguous run of tiles, row-major
 // in the image, so consecutive tiles share halo columns in L2) and all 32 x 32 channels.  Per
 // tile the block stages the 10 x 10 halo of gy and of the activation into LDS as fp16 pieces
-// (pixel-major records, 96-B rows), software-pipelined like wgrad_pipe_kernel: the items of
-// tile t+1 are transformed and written between the MFMAs of tile t while their registers are
-// refilled with tile t+2's loads.  Eight waves:
+// (pixel-major records, 96-B rows), double-buffered: four staging waves transform, split and
+// write tile t+1 while their registers refill with tile t+2's loads, beside eight MFMA waves on
+// tile t (one barrier per tile; DW_NOSPEC: the round-5 first form, where the MFMA waves stage
+// between their taps).  MFMA waves:
 //   weight gradient: wave w owns the (co 16 x ci 16) block (w & 1, (w >> 1) & 1) for the tile's
 //     pixels 32 (w >> 2) .. +31 (one k-step of v_mfma_f32_16x16x32_f16 per tap; the two pixel
 //     halves are folded at the end), operands by transposed LDS reads (ds_read_b64_tr_b16);
 //   input gradient: wave w owns output pixels 16 (w & 3) .. +15 x ci 16 (w >> 2): per tap one
 //     K = 32 (all gy channels) MFMA, A = the gy halo shifted by the tap (ds_read_b128), B = the
-//     weight pack (staged through LDS once, then held in registers).
+//     weight pack (resident in LDS; DW_NOSPEC: in registers).
 // Each tap's LDS operands are read during the previous tap's MFMAs (one tap ahead).
 // Both run the split-fp16 products a1 b0 + a0 b1 + a0 b0 (f16x3).  The gy operand carries one
 // power-of-two scale per slice (from the applies' per-tile maxima, as the weight gradient's), the
@@ -52,9 +53,9 @@ constexpr int DW_PIECE = DW_HALO * DW_RS;          // one fp16 piece image
 constexpr int DW_IMG = 2 * DW_PIECE;               // two pieces
 constexpr int DW_BUF = 2 * DW_IMG;                 // gy image + activation image
 constexpr int DW_WPACK = 4 * 10 * 2 * DW_C * 8 * 2;  // the dgrad pack (4 chunks x 10 taps x 2 pieces)
-constexpr int DW_NTH = 512;
+constexpr int DW_NTH = 512;       // the MFMA waves
+constexpr int DW_NTH_SPEC = 768;  // SPEC: + 4 staging waves
 constexpr int DW_ITEMS = DW_HALO * (DW_C / 4);     // float4 items of one halo tensor
-constexpr int DW_K = (DW_ITEMS + DW_NTH - 1) / DW_NTH;   // items per thread per tensor (2)
 constexpr size_t DW_LDS = (size_t)DW_WPACK + 2 * (size_t)DW_BUF + 4096;
 
 typedef short dw_s16x4 __attribute__((ext_vector_type(4)));
@@ -100,8 +101,12 @@ struct DwGeom {
 
 // UPS: the source is at H/2 x W/2 (decoder.13: ACT_NORM_UP, the input gradient summed over 2x2
 // windows, FP_UPSUM); else the same resolution (encoder.1: ACT_NORM, P_ID)
-template <bool UPS>
-__global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
+// SPEC (round 5): 4 more waves (768 threads) do all the staging -- item loads, normalisation, fp16
+// split, LDS stores, bias sums -- so the 8 MFMA waves run their taps without it and the staging
+// VALU can issue beside their MFMAs on the same SIMDs; the input-gradient weights are then read
+// from LDS per tap (the 168-VGPR budget of three waves per SIMD has no room for them)
+template <bool UPS, bool SPEC>
+__global__ __launch_bounds__(SPEC ? DW_NTH_SPEC : DW_NTH, 1) void dwgrad_fused_kernel(
     const float* __restrict__ gy, const float* __restrict__ gmax, int gmT,
     const char* __restrict__ wpack, const float* __restrict__ yprev, const float2* __restrict__ stp,
     float* __restrict__ hout, double2* __restrict__ ipart, float* __restrict__ wpart,
@@ -117,9 +122,13 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
   const int Hs = UPS ? H / 2 : H, Ws = UPS ? W / 2 : W;
   const int per_img = g.ntx * g.ntx;
   constexpr int C = DW_C;
+  constexpr int NTH = SPEC ? DW_NTH_SPEC : DW_NTH;   // threads
+  constexpr int NST = SPEC ? NTH - DW_NTH : DW_NTH;  // staging threads
+  constexpr int KS = (DW_ITEMS + NST - 1) / NST;     // items per staging thread per tensor
+  const bool stager = SPEC && wave >= DW_NTH / 64;   // wave-uniform
 
   // ---- the dgrad weight pack -> LDS (resident), its layer shift from the trailer
-  for (int i = tid; i < DW_WPACK / 16; i += DW_NTH)
+  for (int i = tid; i < DW_WPACK / 16; i += NTH)
     reinterpret_cast<float4*>(lw)[i] = reinterpret_cast<const float4*>(wpack)[i];
   const int wshift = *reinterpret_cast<const int*>(wpack + DW_WPACK);
   // the slice's gy scale (its images' maxima), shared by both contractions
@@ -131,14 +140,15 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
   // ---- item geometry (tile-invariant): item k of this thread is halo pixel hp = (tid + 512 k)
   // / 8 of the tile (row hr, column hc, -1 .. 8), channels 4 qd .. 4 qd + 3.  The same items
   // stage gy (this block's output gradient) and the activation source.
-  const int qd = tid & 7;
-  int hrc[DW_K], ldo[DW_K], gyo[DW_K], sro[DW_K];
-  bool live[DW_K], inner[DW_K];
+  const int sid = SPEC ? tid - DW_NTH : tid;   // staging thread index (SPEC: waves 8-11)
+  const int qd = sid & 7;
+  int hrc[KS], ldo[KS], gyo[KS], sro[KS];
+  bool live[KS], inner[KS];
 #pragma unroll
-  for (int k = 0; k < DW_K; ++k) {
+  for (int k = 0; k < KS; ++k) {
     // pixel ranks with bits 0 / 1 swapped: each 16-lane group of a ds_write_b64 stores pixels
     // p, p + 2 (conflict-free, conv_wgrad.hip wg_store_perm)
-    int hp = (tid + DW_NTH * k) >> 3;
+    int hp = (sid + NST * k) >> 3;
     hp = (hp & ~3) | ((hp >> 1) & 1) | ((hp & 1) << 1);
     live[k] = hp < DW_HALO;
     const int hr = hp / DW_HP - 1, hc = hp % DW_HP - 1;
@@ -158,7 +168,7 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
     x0 = (rr & (g.ntx - 1)) * DW_TS;
   };
   // registers: gy and activation items of the loading tile (l*) and stats of the staging tile (s*)
-  float4 rg[DW_K], ra[DW_K];
+  float4 rg[KS], ra[KS];
   float2 fl[4], fs[4];   // {rstd, -mean*rstd} of the item channels, loading / staging tile image
   int lb = 0, ly = 0, lx = 0, sy = 0, sx = 0;
   auto issue = [&](int t) EV_LAMBDA_INLINE {
@@ -168,7 +178,7 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
     const int goff = (ly * W + lx) * C * 4;
     const int soff = UPS ? ((ly >> 1) * Ws + (lx >> 1)) * C * 4 : goff;
 #pragma unroll
-    for (int k = 0; k < DW_K; ++k) {
+    for (int k = 0; k < KS; ++k) {
       // rows above / below the image fall outside the descriptor range (read 0); the left /
       // right halo columns read a neighbouring row, zeroed at staging (dead items: out of range)
       const int o = live[k] ? goff + gyo[k] : (int)0x80000000;
@@ -241,14 +251,16 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
     if constexpr (!UPS) {
       const float* yp = yprev + (((size_t)b0 * H + y0 + rr) * W + x0 + cc) * C + eci;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pv[r] = __builtin_nontemporal_load(yp + r * C);
+      // default policy: the other ci block's wave reads the other half of each 128-B line
+      // (non-temporal half-line loads fetched lines twice: -20 us with the default)
+      for (int r = 0; r < 4; ++r) pv[r] = yp[r * C];
     } else {
       // lanes gq < 2 own the windows (wr, wc), (wr, wc + 1) at H/2 x W/2; the others load the
       // same addresses (no divergent branch, the values are unused)
       const int wr = (y0 >> 1) + (rr >> 1), wc = (x0 >> 1) + ((cc & 4) >> 1);
       const float* yp = yprev + (((size_t)b0 * (H >> 1) + wr) * (W >> 1) + wc) * C + eci;
-      pv[0] = __builtin_nontemporal_load(yp);
-      pv[1] = __builtin_nontemporal_load(yp + C);
+      pv[0] = yp[0];
+      pv[1] = yp[C];
       pv[2] = pv[3] = 0.f;
     }
   };
@@ -282,7 +294,7 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
         const float ga = y > sp.x ? v : v * kSlope;
         s1 += ga;
         s2 = fmaf(ga, x, s2);
-        __builtin_nontemporal_store(ga, hp + r * C);
+        hp[r * C] = ga;   // half lines: the L2 merges the two ci blocks' halves
       }
       s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
       s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
@@ -303,7 +315,7 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
           const float ga = y > sp.x ? gs[j] : gs[j] * kSlope;
           s1 += ga;
           s2 = fmaf(ga, x, s2);
-          __builtin_nontemporal_store(ga, hp + j * C);
+          hp[j * C] = ga;
         }
       }
       s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
@@ -315,22 +327,45 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
   };
 
   // ---- prologue: tile t_beg staged into set 0, tile t_beg + 1 (clamped) in the registers
-  issue(t_beg);
-  shift();
+  const bool stages = !SPEC || stager;   // this wave stages
+  if (stages) {
+    issue(t_beg);
+    shift();
+  }
   __syncthreads();   // the weight pack is in LDS before anyone reads it (and before set 0 is read)
+  if (stages) {
 #pragma unroll
-  for (int k = 0; k < DW_K; ++k) stage(k, lbuf);
-  bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
-  issue(min(t_beg + 1, t_end - 1));
+    for (int k = 0; k < KS; ++k) stage(k, lbuf);
+    bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
+    issue(min(t_beg + 1, t_end - 1));
+  }
   __syncthreads();
 
   // the input-gradient B fragments of this lane (the pack: 9 taps x 2 pieces) stay in registers
   // for the whole slice (72 VGPRs; read once instead of once per tile: -30 us at B = 256)
   f16x8 dbr[9][2];
+  if constexpr (!SPEC) {
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
+    for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) dbr[tap][i] = dw_frag(lw + ((((gq * 10 + tap) * 2 + i) * C) + eci) * 16);
+      for (int i = 0; i < 2; ++i) dbr[tap][i] = dw_frag(lw + ((((gq * 10 + tap) * 2 + i) * C) + eci) * 16);
+  }
+  if (stager) {
+    // SPEC staging waves (their own loop, so their registers are not live beside the MFMA
+    // waves' accumulators): tile t+1 into the other set, then its registers refill with t+2
+    for (int t = t_beg; t < t_end; ++t) {
+      char* nbuf = lbuf + (1 - ((t - t_beg) & 1)) * DW_BUF;
+      shift();
+      tb = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) stage(k, nbuf);
+      issue(min(t + 2, t_end - 1));
+      const float keep = (t + 1 < t_end) ? 1.f : 0.f;
+      bs[0] += (double)(tb.x * keep); bs[1] += (double)(tb.y * keep);
+      bs[2] += (double)(tb.z * keep); bs[3] += (double)(tb.w * keep);
+      __syncthreads();
+    }
+  } else {
   for (int t = t_beg; t < t_end; ++t) {
     const int cur = (t - t_beg) & 1;
     const char* gimgp = lbuf + cur * DW_BUF;
@@ -338,8 +373,10 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
     char* nbuf = lbuf + (1 - cur) * DW_BUF;
     pre_load(t);
     if (t > t_beg && tid < C) combine(t - 1);   // the previous tile's slot sums (behind its barrier)
-    shift();
-    tb = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (!SPEC) {
+      shift();
+      tb = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     // weight-gradient A fragments (gy, k = this wave's 32 pixels): one read per piece
     f16x8 wa[2];
 #pragma unroll
@@ -367,7 +404,12 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
       __builtin_amdgcn_sched_barrier(0);   // issued ahead of this tap's MFMAs
       const f16x8* wb = wbc;
       const f16x8* da = dac;
-      const f16x8* db = dbr[tap];
+      f16x8 dbt[2];
+      if constexpr (SPEC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dbt[i] = dw_frag(lw + ((((gq * 10 + tap) * 2 + i) * C) + eci) * 16);
+      }
+      const f16x8* db = SPEC ? dbt : dbr[tap];
       accw[tap] = dw_mfma(wa[1], wb[0], accw[tap]);
       accw[tap] = dw_mfma(wa[0], wb[1], accw[tap]);
       accw[tap] = dw_mfma(wa[0], wb[0], accw[tap]);
@@ -376,11 +418,13 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
       accd = dw_mfma(da[0], db[0], accd);
       // staging of tile t+1 between the taps (item k at tap 2 k + 1), then its register
       // refill is tile t+2's load (issued once, after the last item)
-      dw_for<DW_K>([&](auto k_c) EV_LAMBDA_INLINE {
-        constexpr int k = decltype(k_c)::value;
-        if constexpr (tap == 2 * k + 1) stage(k, nbuf);
-      });
-      if constexpr (tap == 2 * DW_K) issue(min(t + 2, t_end - 1));
+      if constexpr (!SPEC) {
+        dw_for<KS>([&](auto k_c) EV_LAMBDA_INLINE {
+          constexpr int k = decltype(k_c)::value;
+          if constexpr (tap == 2 * k + 1) stage(k, nbuf);
+        });
+        if constexpr (tap == 2 * KS) issue(min(t + 2, t_end - 1));
+      }
       if constexpr (tap < 8) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) { wbc[i] = wbn[i]; dac[i] = dan[i]; }
@@ -391,7 +435,7 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
     // first VALU read of the last MFMA's result right behind the branch on the skipping path,
     // without the wait states an MFMA result needs (wrong input gradients on every slice's last
     // tile, tools/debug/dw_ups.py)
-    {
+    if constexpr (!SPEC) {
       const float keep = (t + 1 < t_end) ? 1.f : 0.f;
       bs[0] += (double)(tb.x * keep); bs[1] += (double)(tb.y * keep);
       bs[2] += (double)(tb.z * keep); bs[3] += (double)(tb.w * keep);
@@ -401,11 +445,12 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
     accd = dw_f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
   }
+  }
   if (tid < C) combine(t_end - 1);
 
   // ---- weight-gradient partials: fold the two pixel halves (waves 4-7 into 0-3) through LDS
   float* xs = reinterpret_cast<float*>(lbuf);   // LDS sets are free after the last barrier
-  if (wks == 1) {
+  if (wks == 1) {   // waves 4-7 (SPEC staging waves: wks == 2)
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -426,12 +471,12 @@ __global__ __launch_bounds__(DW_NTH, 1) void dwgrad_fused_kernel(
   // bias partial: threads with the same channel group qd fold their sums in a fixed order
   double* xb = reinterpret_cast<double*>(lbuf);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) xb[i * DW_NTH + tid] = bs[i];
+  for (int i = 0; i < 4; ++i) xb[i * NTH + tid] = bs[i];
   __syncthreads();
   if (tid < C) {
     const int qq = tid >> 2, i = tid & 3;
     double sum = 0.0;
-    for (int m = qq; m < DW_NTH; m += 8) sum += xb[i * DW_NTH + m];
+    for (int m = qq; m < NTH; m += 8) sum += xb[i * NTH + m];
     bpart[(size_t)slice * C + tid] = (float)sum;
   }
 }
@@ -479,26 +524,18 @@ extern "C" int ebsdvae_conv3x3_dwgrad_f16(const float* gy, const float* gmax, in
   EV_REQUIRE(cin == DW_C && cout == DW_C && dw_geom(B, H, W, &g),
              "conv3x3_dwgrad_f16: unsupported shape B=%d H=%d W=%d cin=%d cout=%d", B, H, W, cin, cout);
   hipStream_t s = (hipStream_t)stream;
-  if (src_mode == ACT_NORM) {
-    static bool once = false;
-    if (!once) {
-      (void)hipFuncSetAttribute((const void*)dwgrad_fused_kernel<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)DW_LDS);
-      once = true;
-    }
-    hipLaunchKernelGGL(dwgrad_fused_kernel<false>, dim3(g.slices), dim3(DW_NTH), DW_LDS, s, gy, gmax,
-                       gm_tiles, (const char*)wpack, y_prev, (const float2*)st_prev, gin,
-                       (double2*)part, wpart, bpart, B, H, W, g);
-  } else {
-    static bool once = false;
-    if (!once) {
-      (void)hipFuncSetAttribute((const void*)dwgrad_fused_kernel<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)DW_LDS);
-      once = true;
-    }
-    hipLaunchKernelGGL(dwgrad_fused_kernel<true>, dim3(g.slices), dim3(DW_NTH), DW_LDS, s, gy, gmax,
-                       gm_tiles, (const char*)wpack, y_prev, (const float2*)st_prev, gin,
-                       (double2*)part, wpart, bpart, B, H, W, g);
-  }
+  auto launch = [&](auto kern, int nth) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DW_LDS);
+    hipLaunchKernelGGL(kern, dim3(g.slices), dim3(nth), DW_LDS, s, gy, gmax, gm_tiles,
+                       (const char*)wpack, y_prev, (const float2*)st_prev, gin, (double2*)part, wpart,
+                       bpart, B, H, W, g);
+  };
+#ifdef DW_NOSPEC   // A/B: every wave stages between its taps (no staging waves)
+  if (src_mode == ACT_NORM) launch(dwgrad_fused_kernel<false, false>, DW_NTH);
+  else launch(dwgrad_fused_kernel<true, false>, DW_NTH);
+#else
+  if (src_mode == ACT_NORM) launch(dwgrad_fused_kernel<false, true>, DW_NTH_SPEC);
+  else launch(dwgrad_fused_kernel<true, true>, DW_NTH_SPEC);
+#endif
   return evh::check_launch("conv3x3_dwgrad_f16");
 }
