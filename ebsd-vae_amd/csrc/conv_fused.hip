@@ -168,47 +168,53 @@ __global__ __launch_bounds__(SPEC ? DW_NTH_SPEC : DW_NTH, 1) void dwgrad_fused_k
     x0 = (rr & (g.ntx - 1)) * DW_TS;
   };
   // registers: gy and activation items of the loading tile (l*) and stats of the staging tile (s*)
-  float4 rg[KS], ra[KS];
-  float2 fl[4], fs[4];   // {rstd, -mean*rstd} of the item channels, loading / staging tile image
-  int lb = 0, ly = 0, lx = 0, sy = 0, sx = 0;
-  auto issue = [&](int t) EV_LAMBDA_INLINE {
-    tile_at(t, lb, ly, lx);
-    const auto rgy = __builtin_amdgcn_make_buffer_rsrc((void*)(gy + (size_t)lb * H * W * C), 0, gimg, 0x00020000);
-    const auto rsr = __builtin_amdgcn_make_buffer_rsrc((void*)(yprev + (size_t)lb * Hs * Ws * C), 0, simg, 0x00020000);
-    const int goff = (ly * W + lx) * C * 4;
-    const int soff = UPS ? ((ly >> 1) * Ws + (lx >> 1)) * C * 4 : goff;
+  // two register slots (SPEC staging waves: tile u's loads are issued two tiles before it is
+  // staged; the MFMA waves' in-tap staging uses slot 0 only)
+  float4 rg[2][KS], ra[2][KS];
+  float2 fl[2][4], fs[4];   // {rstd, -mean*rstd} of the item channels, loading / staging tile image
+  int lb[2] = {0, 0}, ly[2] = {0, 0}, lx[2] = {0, 0}, sy = 0, sx = 0;
+  auto issue = [&](int t, auto sl_c) EV_LAMBDA_INLINE {
+    constexpr int sl = decltype(sl_c)::value;
+    tile_at(t, lb[sl], ly[sl], lx[sl]);
+    const int lb_ = lb[sl], ly_ = ly[sl], lx_ = lx[sl];
+    const auto rgy = __builtin_amdgcn_make_buffer_rsrc((void*)(gy + (size_t)lb_ * H * W * C), 0, gimg, 0x00020000);
+    const auto rsr = __builtin_amdgcn_make_buffer_rsrc((void*)(yprev + (size_t)lb_ * Hs * Ws * C), 0, simg, 0x00020000);
+    const int goff = (ly_ * W + lx_) * C * 4;
+    const int soff = UPS ? ((ly_ >> 1) * Ws + (lx_ >> 1)) * C * 4 : goff;
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       // rows above / below the image fall outside the descriptor range (read 0); the left /
       // right halo columns read a neighbouring row, zeroed at staging (dead items: out of range)
       const int o = live[k] ? goff + gyo[k] : (int)0x80000000;
       const int so = live[k] ? soff + sro[k] : (int)0x80000000;
-      rg[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rgy, o, 0, 0));
-      ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsr, so, 0, 0));
+      rg[sl][k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rgy, o, 0, 0));
+      ra[sl][k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsr, so, 0, 0));
     }
-    const float4* sp = reinterpret_cast<const float4*>(stp + (size_t)lb * C + qd * 4);
+    const float4* sp = reinterpret_cast<const float4*>(stp + (size_t)lb_ * C + qd * 4);
     const float4 u0 = sp[0], u1 = sp[1];
-    fl[0] = norm_fs(make_float2(u0.x, u0.y)); fl[1] = norm_fs(make_float2(u0.z, u0.w));
-    fl[2] = norm_fs(make_float2(u1.x, u1.y)); fl[3] = norm_fs(make_float2(u1.z, u1.w));
+    fl[sl][0] = norm_fs(make_float2(u0.x, u0.y)); fl[sl][1] = norm_fs(make_float2(u0.z, u0.w));
+    fl[sl][2] = norm_fs(make_float2(u1.x, u1.y)); fl[sl][3] = norm_fs(make_float2(u1.z, u1.w));
   };
-  auto shift = [&]() EV_LAMBDA_INLINE {
-    sy = ly; sx = lx;
+  auto shift = [&](auto sl_c) EV_LAMBDA_INLINE {
+    constexpr int sl = decltype(sl_c)::value;
+    sy = ly[sl]; sx = lx[sl];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fs[i] = fl[i];
+    for (int i = 0; i < 4; ++i) fs[i] = fl[sl][i];
   };
   float4 tb = make_float4(0.f, 0.f, 0.f, 0.f);   // this thread's gy sums of the staging tile (bias)
   double bs[4] = {0.0, 0.0, 0.0, 0.0};
   // stage item k (gy and activation) of the staging tile into set buf
-  auto stage = [&](int k, char* buf) EV_LAMBDA_INLINE {
+  auto stage = [&](int k, char* buf, auto sl_c) EV_LAMBDA_INLINE {
+    constexpr int sl = decltype(sl_c)::value;
     if (!live[k]) return;
     const int hr = (hrc[k] >> 8) - 1, hc = (hrc[k] & 255) - 1;
     const bool in = (unsigned)(sy + hr) < (unsigned)H && (unsigned)(sx + hc) < (unsigned)W;
-    float4 v = in ? rg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = in ? rg[sl][k] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (inner[k]) { tb.x += v.x; tb.y += v.y; tb.z += v.z; tb.w += v.w; }
     dw_store(buf + ldo[k], v, gsc);
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     if (in) {
-      const float4 r = ra[k];
+      const float4 r = ra[sl][k];
       a = make_float4(normact_fs(r.x, fs[0]), normact_fs(r.y, fs[1]), normact_fs(r.z, fs[2]),
                       normact_fs(r.w, fs[3]));
     }
@@ -327,17 +333,27 @@ __global__ __launch_bounds__(SPEC ? DW_NTH_SPEC : DW_NTH, 1) void dwgrad_fused_k
   };
 
   // ---- prologue: tile t_beg staged into set 0, tile t_beg + 1 (clamped) in the registers
-  const bool stages = !SPEC || stager;   // this wave stages
-  if (stages) {
-    issue(t_beg);
-    shift();
+  const std::integral_constant<int, 0> S0;
+  const std::integral_constant<int, 1> S1;
+  if (stager) {             // SPEC: tiles t_beg, t_beg + 1 into slots 0, 1
+    issue(t_beg, S0);
+    issue(min(t_beg + 1, t_end - 1), S1);
+  } else if (!SPEC) {
+    issue(t_beg, S0);
+    shift(S0);
   }
   __syncthreads();   // the weight pack is in LDS before anyone reads it (and before set 0 is read)
-  if (stages) {
+  if (stager) {
+    shift(S0);
 #pragma unroll
-    for (int k = 0; k < KS; ++k) stage(k, lbuf);
+    for (int k = 0; k < KS; ++k) stage(k, lbuf, S0);
     bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
-    issue(min(t_beg + 1, t_end - 1));
+    issue(min(t_beg + 2, t_end - 1), S0);
+  } else if (!SPEC) {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) stage(k, lbuf, S0);
+    bs[0] += (double)tb.x; bs[1] += (double)tb.y; bs[2] += (double)tb.z; bs[3] += (double)tb.w;
+    issue(min(t_beg + 1, t_end - 1), S0);
   }
   __syncthreads();
 
@@ -353,17 +369,22 @@ __global__ __launch_bounds__(SPEC ? DW_NTH_SPEC : DW_NTH, 1) void dwgrad_fused_k
   if (stager) {
     // SPEC staging waves (their own loop, so their registers are not live beside the MFMA
     // waves' accumulators): tile t+1 into the other set, then its registers refill with t+2
-    for (int t = t_beg; t < t_end; ++t) {
+    // tile t+1 is in slot (t + 1 - t_beg) & 1; its slot refills with tile t+3
+    auto stager_tile = [&](int t, auto sl_c) EV_LAMBDA_INLINE {
       char* nbuf = lbuf + (1 - ((t - t_beg) & 1)) * DW_BUF;
-      shift();
+      shift(sl_c);
       tb = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int k = 0; k < KS; ++k) stage(k, nbuf);
-      issue(min(t + 2, t_end - 1));
+      for (int k = 0; k < KS; ++k) stage(k, nbuf, sl_c);
+      issue(min(t + 3, t_end - 1), sl_c);
       const float keep = (t + 1 < t_end) ? 1.f : 0.f;
       bs[0] += (double)(tb.x * keep); bs[1] += (double)(tb.y * keep);
       bs[2] += (double)(tb.z * keep); bs[3] += (double)(tb.w * keep);
       __syncthreads();
+    };
+    for (int t = t_beg; t < t_end; t += 2) {
+      stager_tile(t, S1);
+      if (t + 1 < t_end) stager_tile(t + 1, S0);
     }
   } else {
   for (int t = t_beg; t < t_end; ++t) {
@@ -374,7 +395,7 @@ __global__ __launch_bounds__(SPEC ? DW_NTH_SPEC : DW_NTH, 1) void dwgrad_fused_k
     pre_load(t);
     if (t > t_beg && tid < C) combine(t - 1);   // the previous tile's slot sums (behind its barrier)
     if constexpr (!SPEC) {
-      shift();
+      shift(S0);
       tb = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // weight-gradient A fragments (gy, k = this wave's 32 pixels): one read per piece
@@ -421,9 +442,9 @@ __global__ __launch_bounds__(SPEC ? DW_NTH_SPEC : DW_NTH, 1) void dwgrad_fused_k
       if constexpr (!SPEC) {
         dw_for<KS>([&](auto k_c) EV_LAMBDA_INLINE {
           constexpr int k = decltype(k_c)::value;
-          if constexpr (tap == 2 * k + 1) stage(k, nbuf);
+          if constexpr (tap == 2 * k + 1) stage(k, nbuf, S0);
         });
-        if constexpr (tap == 2 * KS) issue(min(t + 2, t_end - 1));
+        if constexpr (tap == 2 * KS) issue(min(t + 2, t_end - 1), S0);
       }
       if constexpr (tap < 8) {
 #pragma unroll
