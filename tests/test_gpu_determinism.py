@@ -68,3 +68,18 @@ def test_repeated_steps_are_bitwise_equal(cuda, prec, name, copies):
                 off += k
     print(f"\n[{prec} {name} x{copies}] {REPEATS} repeats; differences: {bad[:12]}")
     assert not bad, bad
+
+
+def test_fused_input_weight_gradient_steps_are_bitwise_equal(cuda, monkeypatch):
+    """The opt-in fused input + weight gradient (EBSDVAE_DWFUSE=1: staging waves, two-slot
+    prefetch, fixed-order slot / slice sums) is as run-to-run deterministic as the default."""
+    monkeypatch.setattr(E, "_DWFUSE", True)
+    m, x, eps, kl = _trainer("vae128_b4", cuda, 64)
+    with E.precision("f16x3"):
+        with E.record_launches() as launches:
+            tr, outs = _repeat_steps(m, x, eps, kl)
+    assert "ebsdvae_conv3x3_dwgrad_f16" in launches   # the fused kernel ran
+    l0, g0 = outs[0]
+    assert torch.isfinite(g0).all()
+    for li, gi in outs[1:]:
+        assert torch.equal(li, l0) and torch.equal(gi, g0)
