@@ -16,6 +16,13 @@ import os as _os
 
 __version__ = "0.2.0"
 
+# The training step runs its weight gradients on a second HIP stream; with a data-parallel RCCL
+# group initialised, HIP's default of 4 hardware queues per process makes that stream share a
+# queue with the main one (the step loses its overlap: 8.55 -> 9.30 ms at B = 256, DESIGN.md
+# section 6).  HIP reads the variable when its runtime initialises, so this takes effect when
+# latice is imported before the first GPU call; a value the user set is kept.
+_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 
 def _extend_path(pkg_path, *sub):
     root = _os.environ.get("LATICE_REFERENCE_ROOT")

@@ -2,9 +2,12 @@
 forced on (GradReducer(force=True)), so the step issues every bucket's collective exactly as
 at N > 1 (world 1: RCCL's copy kernels only).  Variants: three buckets (bucket 1 started after
 the deep encoder layers' weight gradients, their slice reductions flushed early) and two
-buckets (the round-4 layout: decoder + heads, then the whole encoder after the backward).
+buckets (the round-4 layout: decoder + heads, then the whole encoder after the backward), and
+no collective at all (the reducer inactive, as at N = 1).
 
     python tools/bucket_ab.py [--steps 20] [--rounds 3]
+    GPU_MAX_HW_QUEUES=8 python tools/bucket_ab.py    # what bench.py and latice set (this script
+                                                     # initialises HIP before importing latice: 4)
 """
 import argparse
 import os
@@ -38,6 +41,7 @@ def main():
     x = torch.from_numpy(synthetic_patterns(0, 256, 128)).to(dev)
     three = (tr._deep_last, tr.reducer)
     two = (None, GradReducer(tr.gflat, tr.split, force=True))
+    none = (None, GradReducer(tr.gflat, tr.split))   # world 1, not forced: no collective
 
     def timed(cfg):
         tr._deep_last, tr.reducer = cfg
@@ -51,8 +55,9 @@ def main():
         return (time.perf_counter() - t0) / args.steps * 1e3
 
     for r in range(args.rounds):
-        a, b = timed(three), timed(two)
-        print(f"round {r}: three buckets {a:.3f} ms/step, two buckets {b:.3f} ms/step", flush=True)
+        a, b, c = timed(three), timed(two), timed(none)
+        print(f"round {r}: three buckets {a:.3f} ms/step, two buckets {b:.3f}, no collective "
+              f"{c:.3f}", flush=True)
     dist.destroy_process_group()
 
 
