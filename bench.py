@@ -134,25 +134,55 @@ def cpu_baseline(plan, timed: int = 3):
 
 
 class _SyntheticPatternLoader:
-    """A DPDataModule test_dataloader stand-in over synthetic raw patterns already in HBM:
-    each batch is the on-device DPdataset transform (ebsdvae_ingest_patterns) of a raw
-    float64 batch, with its angles -- what build_dictionary's loop consumes."""
+    """A DPDataModule test_dataloader stand-in over synthetic raw patterns: each batch is the
+    on-device DPdataset transform (ebsdvae_ingest_patterns) of a raw float64 batch, with its
+    angles -- what build_dictionary's loop consumes.  raw on the device: the batch is already
+    resident in HBM.  raw in pinned host memory (h2d): every batch is first copied host ->
+    device (the reference's `data.to(device)`, latice/index/dp_indexer.py:281, here of the raw
+    float64 batch) on a copy stream, double-buffered so batch i+1's copy runs under batch i's
+    encode."""
 
-    def __init__(self, raw, image_size, nb, angles):
+    def __init__(self, raw, image_size, nb, angles, device=None):
         from latice.data_module import ingest_patterns
         self._ingest = ingest_patterns
         self.raw, self.S, self.nb, self.angles = raw, image_size, nb, angles
+        dev = raw.device if device is None else device
         self.x = torch.empty(raw.shape[0], 1, image_size, image_size, dtype=torch.float32,
-                             device=raw.device)
+                             device=dev)
+        self.h2d = raw.device.type == "cpu"
+        if self.h2d:
+            self.bufs = [torch.empty(raw.shape, dtype=raw.dtype, device=dev) for _ in range(2)]
+            self.copy = torch.cuda.Stream(device=dev)
 
     def __len__(self):
         return self.nb
 
     def __iter__(self):
         B = self.raw.shape[0]
+        if not self.h2d:
+            for i in range(self.nb):
+                yield (self._ingest(self.raw, (self.S, self.S), out=self.x),
+                       torch.from_numpy(self.angles[i * B:(i + 1) * B]))
+            return
+        main = torch.cuda.current_stream(self.x.device)
+        done = [None, None]
+
+        def fetch(i):
+            buf = self.bufs[i % 2]
+            self.copy.wait_stream(main)   # the ingest that last read this buffer is done
+            with torch.cuda.stream(self.copy):
+                buf.copy_(self.raw, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.copy)
+            done[i % 2] = ev
+
+        fetch(0)
         for i in range(self.nb):
-            yield (self._ingest(self.raw, (self.S, self.S), out=self.x),
-                   torch.from_numpy(self.angles[i * B:(i + 1) * B]))
+            main.wait_event(done[i % 2])
+            x = self._ingest(self.bufs[i % 2], (self.S, self.S), out=self.x)
+            if i + 1 < self.nb:
+                fetch(i + 1)
+            yield x, torch.from_numpy(self.angles[i * B:(i + 1) * B])
 
 
 def encoder_latents(model, plan, args, dev, world):
@@ -196,6 +226,35 @@ def encoder_latents(model, plan, args, dev, world):
         dist.barrier()
     el = time.perf_counter() - t0
     finite = bool(np.isfinite(lat).all())
+    # the same loop with every raw float64 batch copied host -> device first (pinned memory,
+    # copy stream, double-buffered): the PCIe-inclusive rate beside the HBM-resident one
+    nh = min(nb, args.c4_h2d_batches)
+    h2d = None
+    if nh > 0:
+        raw_h = raw.cpu().pin_memory()
+        with quiet:
+            ix._extract_latent_vectors_with_angles(_SyntheticPatternLoader(raw_h, S, 2, angles, dev))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        th = time.perf_counter()
+        with quiet:
+            ix._extract_latent_vectors_with_angles(_SyntheticPatternLoader(raw_h, S, nh, angles, dev))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        hel = time.perf_counter() - th
+        if world > 1:
+            t = torch.tensor([hel], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            hel = float(t)
+        h2d = {"value": round(world * B * nh / hel, 1), "unit": "latents/s", "batches": nh,
+               "ms_per_batch": round(hel / nh * 1e3, 3),
+               "raw_batch_mb": round(raw_h.numel() * 8 / 1e6, 1),
+               "what": "the same unmodified loop with each raw float64 batch copied from pinned host "
+                       "memory to the GPU first (dp_indexer.py:281 data.to(device)); copy stream, "
+                       "double-buffered under the previous batch's encode"}
+        del raw_h
     # the encoder-only engine loop without the per-batch host copy, for comparison
     params = dict(model.named_parameters())
     packs = model._inference_packs(params)
@@ -247,6 +306,7 @@ def encoder_latents(model, plan, args, dev, world):
                          "measured_ms_per_batch": round(el / nb * 1e3, 3),
                          "frac": round((conv_att + ingest_att + heads_att) / (el / nb), 4),
                          "engine_only_frac": round((conv_att + ingest_att + heads_att) / (eng / ne), 4)},
+            "with_host_to_device_copy": h2d,
             "engine_only": {"value": round(world * B * ne / eng, 1), "unit": "latents/s",
                             "batches": ne, "what": "transform + encode_latents, no host copy"},
             "query": {"metric": "queries/sec (cosine top-20 over the dictionary + orientation "
@@ -422,7 +482,7 @@ def main():
     ap.add_argument("--image-size", type=int, default=128)
     ap.add_argument("--latent-dim", type=int, default=16)
     ap.add_argument("--cpu-timed", type=int, default=3, help="timed CPU-baseline steps per shape")
-    ap.add_argument("--strict-fp32-steps", type=int, default=8,
+    ap.add_argument("--strict-fp32-steps", type=int, default=20,
                     help="timed steps of the strict fp32-MFMA leg (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="time without per-kernel events")
@@ -432,6 +492,8 @@ def main():
                     help="conv arithmetic (default: the engine default, f16x3)")
     ap.add_argument("--c4-batches", type=int, default=1024,
                     help="encoder-only inference batches of 1024 for the c4 latents/s field (0: skip)")
+    ap.add_argument("--c4-h2d-batches", type=int, default=64,
+                    help="batches of the c4 variant with the host->device copy of each raw batch (0: skip)")
     ap.add_argument("--c5-steps", type=int, default=10,
                     help="timed steps of the c5 leg (256x256, latent 64, batch 128/GPU; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -501,6 +563,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     probed = 0
+    trainer.time_allreduce = world > 1   # one event pair per step around the exposed all-reduce
     for i in range(args.steps):
         if probe is not None and i % args.probe_every == 0:
             # event-bracketed launches on a sample of the timed steps: each event pair costs
@@ -514,6 +577,7 @@ def main():
         else:
             out = trainer.step(x)
     torch.cuda.synchronize()
+    trainer.time_allreduce = False
     step_ctx.__exit__(None, None, None)
     if world > 1:
         dist.barrier()
@@ -531,6 +595,11 @@ def main():
     loss = float(out[0])
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
+    exposed = trainer.allreduce_exposed_ms()
+    if exposed is not None:
+        t = torch.tensor([exposed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        exposed = round(float(t), 4)
 
     roof = None
     fam = {}
@@ -593,6 +662,11 @@ def main():
                    "latent_dim": args.latent_dim, "parallelism": f"dp{world}"},
         "process_group": pg,
         "rank_ms_per_step": rank_ms,
+        "allreduce_exposed_ms": exposed,
+        "allreduce_exposed_what": ("GPU time per step (HIP events, max over ranks) from the end of the "
+                                   "backward to the completion of the last gradient all-reduce: the "
+                                   "exchange time no backward work hid (trainer.py)"
+                                   if exposed is not None else None),
         "rank_spread_pct": (None if rank_ms is None else
                             round(100.0 * (max(rank_ms) - min(rank_ms)) / max(rank_ms), 2)),
         "roofline": roof,

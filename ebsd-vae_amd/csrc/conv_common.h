@@ -166,6 +166,8 @@ struct InBwdFuse {
   float2* st_out = nullptr;      // in-kernel InstanceNorm finalize (pipe_owns_images): forward
   float2* bst_out = nullptr;     // {mean, rstd}, or the previous block's backward {m1, m2}
   double inv_hw = 0.0;           // 1 / (H*W) of the previous block (bst_out)
+  const float* w0 = nullptr;     // ACT_FIRST forward: the first conv's weight (cin,1,3,3) and
+  const float* b0 = nullptr;     // bias, which the staging recomputes y0 from x with
 };
 
 }  // namespace ev

@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
   __syncthreads();
   float v[FIRST_NPT][4];
   float s[4] = {0.f, 0.f, 0.f, 0.f};
-  float* yb = y + ((size_t)b * H * W + (size_t)r0 * W) * FIRST_C + c;
+  float* yb = y ? y + ((size_t)b * H * W + (size_t)r0 * W) * FIRST_C + c : nullptr;
 #pragma unroll
   for (int j = 0; j < FIRST_NPT; ++j) {
     const int p = pr + 32 * j, h = p / W, w = p - h * W;
@@ -279,8 +279,9 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
       s[2 * k] += y2.x;
       s[2 * k + 1] += y2.y;
     }
-    // non-temporal: y0 is read once, by the next conv (first conv 119 -> 113 us, step -0.03 ms)
-    st4_nt(yb + (size_t)p * FIRST_C, make_float4(v[j][0], v[j][1], v[j][2], v[j][3]));
+    // non-temporal: y0 is read once, by the next conv (first conv 119 -> 113 us, step -0.03 ms).
+    // y == NULL: statistics only -- the next conv recomputes y0 from x (ACT_FIRST staging)
+    if (y) st4_nt(yb + (size_t)p * FIRST_C, make_float4(v[j][0], v[j][1], v[j][2], v[j][3]));
   }
   // band statistics per channel, fixed order: the 8 pixel lanes of a wave by a shuffle tree
   // (lanes cg, cg + 8, ..., cg + 56), then the 4 waves through LDS (a serial walk over 32
@@ -336,7 +337,7 @@ extern "C" int ebsdvae_conv_first_stat_tiles(int H, int W) {
 extern "C" int ebsdvae_conv_first_fwd(const float* x, const float* w0, const float* b0, float* y,
                                       float* part, int B, int H, int W, int C,
                                       ebsdvae_stream_t stream) {
-  EV_REQUIRE(x && w0 && y && part && B > 0 && C == FIRST_C,
+  EV_REQUIRE(x && w0 && part && B > 0 && C == FIRST_C,
              "conv_first_fwd: bad args (C must be %d)", FIRST_C);
   const int th = first_rows(W);
   EV_REQUIRE(th > 0 && FIRST_PX % W == 0 && H % th == 0,

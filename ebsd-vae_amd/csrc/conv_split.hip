@@ -45,6 +45,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int XCK = 8;      // input channels per chunk
+// Source mode of the pipelined kernel only (not an ActMode of the ABI): the input is the first
+// block's activation lrelu(IN(y0)) with y0 = conv(x, w0) + b0 recomputed from the image x while
+// the halo is staged (ebsdvae_conv3x3_fwd_split_first), so y0 is never read
+constexpr int ACT_FIRST = 5;
+constexpr int FIRST_WTAB = 8 * 10 * 4;   // [chunk * 2 + half][tap 0..8, bias][4 channels] floats
 constexpr int XTAPS = 10;   // 9 taps + one zero tap
 constexpr int XPS = 48;     // halo pixel record (bytes)
 #ifndef EV_PIPE_EPI_G
@@ -639,13 +644,14 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 //   and stay resident (Cin = 32 layers, where they fit beside the halo buffers): no weight
 //   DMA per iteration (its issue cost sits in every iteration's instruction stream)
 template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI, int WR>
-__global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
+__global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, const char* __restrict__ wp,
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
     float* __restrict__ act_out, int B, int H, int W, int Cin, int TH, int tpb,
     const float* __restrict__ yprev, const float2* __restrict__ stprev, double2* __restrict__ ipart,
     float* __restrict__ ypool, const float* __restrict__ gmax, int gmT, float2* __restrict__ st_out,
-    float2* __restrict__ bst_out, double fin_inv_hw) {
+    float2* __restrict__ bst_out, double fin_inv_hw, const float* __restrict__ w0,
+    const float* __restrict__ b0) {
   constexpr int WN = NWV / WM;
   constexpr int NT = WN * NF * 32;               // == Cout
   constexpr int MW = MF * 32;
@@ -654,7 +660,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr int WPER = pipe_dma_per(WSLAB, NWV);  // 1-KiB weight pieces per wave per chunk
   constexpr int WSLABP = WPER * NWV * 1024;       // LDS weight buffer (padded to whole rounds)
   constexpr bool POOL = (MODE == ACT_NORM_POOL);
-  constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_POOL || MODE == ACT_NORM_UP);
+  // ACT_FIRST: staged like ACT_NORM (statistics, edge-row mask), its pre-norm values computed
+  // from x instead of loaded (the block's LDS holds the tile's x rows and the first conv's taps)
+  constexpr bool FIRST = (MODE == ACT_FIRST);
+  constexpr bool NORM = (MODE == ACT_NORM || MODE == ACT_NORM_POOL || MODE == ACT_NORM_UP || FIRST);
   constexpr bool UPS = (MODE == ACT_UP || MODE == ACT_NORM_UP);
   constexpr int NR = POOL ? 4 : 1;
   constexpr bool GS = (NP == NP_F16 && MODE == ACT_RAW);   // per-image gradient scale
@@ -664,6 +673,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   constexpr int NLD = KX * NR + (NORM ? 2 : 0);
   static_assert(PD == 1 || NLD <= 15, "pipe_barrier: vmcnt range");
   static_assert(WR == 0 || (PD == 2 && NI == 1), "resident weights: single-image, prefetch 2");
+  static_assert(!FIRST || (WR > 0 && NI == 1), "ACT_FIRST: the resident-weight single-image form");
   extern __shared__ __attribute__((aligned(16))) char xsm[];
   // a tile is TH rows of one image, or NI whole images (NI > 1: TH == H); NI is a template
   // parameter so the single-image kernels carry none of the per-image bookkeeping
@@ -673,6 +683,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   const int xslab = (pixP + 1) * XPS;
   char* lw0 = xsm;
   char* lx0 = xsm + (WR ? WR * WSLAB : 2 * WSLABP);
+  // ACT_FIRST: two x tiles (tile parity) of TH + 4 rows x W + 2 columns (zero columns at -1 and
+  // W, zero rows outside the image), then the first conv's tap table
+  const int XTS = FIRST ? (TH + 4) * (W + 2) : 0;
+  float* xtl = reinterpret_cast<float*>(lx0 + 2 * xslab);
+  const float4* wtab = reinterpret_cast<const float4*>(xtl + 2 * XTS);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -725,6 +740,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   // record offset (dead items write the dummy record pixP)
   const int NIT = (TH + 2) * W;   // staged items (pixels) per image of the tile
   int hm1[KX], boff[KX], ldo[KX];
+  int xoff[FIRST ? KX : 1];        // ACT_FIRST: top-left of the item's 3x3 x window in the x tile
   const int rowb = Ws * Cin * 4;   // bytes per source row
 #pragma unroll
   for (int k = 0; k < KX; ++k) {
@@ -732,6 +748,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     const bool in = pixl < NIT;
     const int hh = pixl / W, c = pixl - hh * W;
     const int r = hh - 1;
+    // halo row hh is image row h0 + hh - 1; its window rows h0 + hh - 2 .. h0 + hh are x-tile
+    // rows hh .. hh + 2, its columns c - 1 .. c + 1 padded columns c .. c + 2
+    if constexpr (FIRST) xoff[k] = in ? hh * (W + 2) + c : 0;
     int o;
     if (POOL) o = 2 * r * rowb + 2 * c * Cin * 4;
     else if (UPS) o = (r >> 1) * rowb + (c >> 1) * Cin * 4;
@@ -757,6 +776,27 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
   int edge[PD];                    // MASK: the slot's tile touches the image top / bottom
   int sb0[PD], sh0[PD], sch[PD];   // tile image / first row / chunk of the slot's data
   float gsc[PD];                   // GS: the slot image's gradient scale
+  int sxb[PD];                     // ACT_FIRST: x-tile buffer (tile parity) of the slot's tile
+  constexpr int XTN = 4;           // ACT_FIRST: x-tile elements per thread (TH + 4) * (W + 2) / threads
+  float xtr[XTN];
+  int xt_pend = -1;                // ACT_FIRST: x-tile buffer to write at the end of the iteration
+  auto load_xtile = [&](int b, int h0) EV_LAMBDA_INLINE {
+    const float* xb = src + (size_t)b * H * W;
+#pragma unroll
+    for (int j = 0; j < XTN; ++j) {
+      const int i = tid + NWV * 64 * j;
+      const int r = i / (W + 2), cc = i - r * (W + 2);
+      const int gh = h0 - 2 + r, gw = cc - 1;
+      xtr[j] = (i < XTS && gh >= 0 && gh < H && gw >= 0 && gw < W) ? xb[gh * W + gw] : 0.f;
+    }
+  };
+  auto store_xtile = [&](int buf) EV_LAMBDA_INLINE {
+#pragma unroll
+    for (int j = 0; j < XTN; ++j) {
+      const int i = tid + NWV * 64 * j;
+      if (i < XTS) xtl[buf * XTS + i] = xtr[j];
+    }
+  };
   int gs_b = -1;                   // GS: image whose shift gs_k holds
   int gs_k = 0;
   auto gshift = [&](int b) EV_LAMBDA_INLINE {
@@ -790,6 +830,16 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     sb0[sl] = b0; sh0[sl] = h0; sch[sl] = ch;
     // GS: the scale of the image this wave stages (NI > 1: one image per wave group)
     if constexpr (GS) gsc[sl] = ldexpf(1.f, gshift(NI == 1 ? b0 : min(b0 + img_u, B - 1)));
+    if constexpr (MASK) edge[sl] = NI > 1 || h0 == 0 || h0 + TH >= H;
+    if constexpr (FIRST) {
+      sxb[sl] = (it >> lgnch) & 1;
+      // a new tile's x rows: loaded now, written to its parity buffer at the end of this
+      // iteration, read from the next iteration's staging on (the prologue writes tile 0's)
+      if (ch == 0 && it > 0) {
+        load_xtile(b0, h0);
+        xt_pend = sxb[sl];
+      }
+    } else {
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)b0 * Hs * Ws * Cin), 0,
                                                       NI == 1 ? img_bytes : img_bytes * min(NI, B - b0),
                                                       0x00020000);
@@ -798,7 +848,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
 #else
     const int toff = (POOL ? 2 * h0 : (UPS ? (h0 >> 1) : h0)) * rowb + ch * XCK * 4;
 #endif
-    if constexpr (MASK) edge[sl] = NI > 1 || h0 == 0 || h0 + TH >= H;
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
       const int vo = boff[k] + toff;
@@ -811,6 +860,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
         raw[sl][k][0] = bload4(rs, vo);
       }
     }
+    }   // !FIRST
     if (NORM) {
       // each lane loads the {mean, rstd} of its own 4-channel half (two 16-byte vector loads;
       // a wave-uniform scalar load would need 3 VALU per value to hand each lane its half)
@@ -836,9 +886,30 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
                       normact_fs(v.w, fs[3]));
     return v;
   };
+  float4 wq[FIRST ? 10 : 1];   // ACT_FIRST: taps 0..8 and the bias of the staged chunk half
   auto stage_item = [&](auto slot_c, int k, const float2 (&fs)[4], char* lx) EV_LAMBDA_INLINE {
     constexpr int sl = decltype(slot_c)::value;
-    float4 v = stage_value(slot_c, k, fs);
+    float4 v;
+    if constexpr (FIRST) {
+      // y0 at the item's pixel for its 4 channels: ebsdvae_conv_first_fwd's own fma chain
+      // (first_conv_px2 per channel pair), then the same normalisation as ACT_NORM
+      const float* xw = xtl + sxb[sl] * XTS + xoff[k];
+      float nb[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) nb[t] = xw[(t / 3) * (W + 2) + t % 3];
+      pkf2 wa[9], wb[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        wa[t] = pk2(wq[t].x, wq[t].y);
+        wb[t] = pk2(wq[t].z, wq[t].w);
+      }
+      const pkf2 ya = first_conv_px2(nb, wa, pk2(wq[9].x, wq[9].y));
+      const pkf2 yb = first_conv_px2(nb, wb, pk2(wq[9].z, wq[9].w));
+      v = make_float4(normact_fs(ya.x, fs[0]), normact_fs(ya.y, fs[1]), normact_fs(yb.x, fs[2]),
+                      normact_fs(yb.y, fs[3]));
+    } else {
+      v = stage_value(slot_c, k, fs);
+    }
     bf16x4 pc[NPC];
     if constexpr (GS)   // the per-image gradient scale folded into the split
       split4_f16_scaled(v, gsc[sl], pc);
@@ -879,6 +950,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     constexpr int sl = decltype(slot_c)::value;
 #pragma unroll
     for (int i = 0; i < 4; ++i) fs[i] = NORM ? norm_fs(st[sl][i]) : make_float2(1.f, 0.f);
+    if constexpr (FIRST) {
+      const float4* wt = wtab + (sch[sl] * 2 + q) * 10;
+#pragma unroll
+      for (int t = 0; t < 10; ++t) wq[t] = wt[t];
+    }
   };
   // weight slab DMA: every wave issues exactly WPER 1-KiB pieces per chunk (the padding
   // pieces of the last chunk fall outside the descriptor's range), so every iteration issues
@@ -1072,6 +1148,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
     kstep(std::integral_constant<int, 3>());
     kstep(std::integral_constant<int, 4>());
     stage_post(std::integral_constant<int, SL_ST>(), fs, lxn);
+    if constexpr (FIRST) {
+      if (xt_pend >= 0) {   // the next tile's x rows, before the barrier that publishes them
+        store_xtile(xt_pend);
+        xt_pend = -1;
+      }
+    }
     EV_TACC(tr_k, tb1);
     EV_T(tb2);
 #ifdef EV_PIPE_NOBAR   // timing experiment only: no barrier (LDS races, wrong results)
@@ -1110,6 +1192,19 @@ __global__ __launch_bounds__(NWV * 64, 2) void conv3x3_pipe_kernel(
       char* d = lx0 + buf * xslab + (img * pixI + row * WP + side * (W + 1)) * XPS + 16 * pc;
       *reinterpret_cast<float4*>(d) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  }
+  if constexpr (FIRST) {
+    // the first conv's taps and bias per (chunk, 4-channel half): [grp][tap 0..8, bias][4]
+    float* wtf = reinterpret_cast<float*>(xtl + 2 * XTS);
+    for (int i = tid; i < FIRST_WTAB; i += NWV * 64) {
+      const int grp = i / 40, rem = i - grp * 40, t = rem >> 2, c = grp * 4 + (rem & 3);
+      wtf[i] = t < 9 ? w0[c * 9 + t] : (b0 ? b0[c] : 0.f);
+    }
+    int xb0, xh0, xch;
+    coords(0, xb0, xh0, xch);
+    load_xtile(xb0, xh0);
+    store_xtile(0);
+    __syncthreads();
   }
   // prologue: weights + halo of it 0 (and the halo of it 1 for PD = 2)
   zero_acc();
@@ -1398,6 +1493,11 @@ static bool pipe_owns_images(const X3Cfg& c, int B, int H, hipStream_t s) {
   return tpb % tpi == 0;
 }
 
+// ACT_FIRST: the two x tiles and the tap table behind the halo buffers
+static size_t first_lds_extra(int TH, int W) {
+  return (2 * (size_t)(TH + 4) * (W + 2) + FIRST_WTAB) * sizeof(float);
+}
+
 template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI, int WR = 0>
 static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const void* wp,
                         const float* bias, float* y, float* part, float* aout, int B, int H, int W,
@@ -1414,9 +1514,11 @@ static void launch_x3_1(const X3Cfg& c, const float* src, const float* st, const
     const int ncu = cu_count(s);
     const int tpb = (ntiles + ncu - 1) / ncu;
     const int nblk = (ntiles + tpb - 1) / tpb;
-    hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), c.lds_pipe, s, src, (const float2*)st,
+    const size_t lds = c.lds_pipe + (MODE == ACT_FIRST ? first_lds_extra(c.TH, W) : 0);
+    hipLaunchKernelGGL(k, dim3(nblk), dim3(NWV * 64), lds, s, src, (const float2*)st,
                        (const char*)wp, bias, y, (float2*)part, aout, B, H, W, cin, c.TH, tpb, f.yprev,
-                       f.stprev, f.part, f.ypool, f.gmax, f.gmT, f.st_out, f.bst_out, f.inv_hw);
+                       f.stprev, f.part, f.ypool, f.gmax, f.gmT, f.st_out, f.bst_out, f.inv_hw, f.w0,
+                       f.b0);
     return;
   }
   if constexpr (NI == 1 && FP != FP_POOLOUT && NP != NP_F16) {
@@ -1719,4 +1821,53 @@ extern "C" int ebsdvae_conv3x3_dgrad_inbwd_f16_bst(const float* g, const float* 
   // (cin, cout) are the conv's: gin and the previous block have cout channels
   return ebsdvae_in_bwd_finalize(part, bst, B, cout, ebsdvae_conv3x3_split_stat_tiles(H, W, cout), prev_hw,
                                  stream);
+}
+
+// The second block's forward with the first block recomputed from x (ACT_FIRST staging):
+// encoder.1 of latice/model.py:111 reading lrelu(IN(conv(x, w0) + b0)) without y0.
+extern "C" int ebsdvae_conv3x3_fwd_split_first_ok(int H, int W, int cin, int cout, int pieces) {
+  X3Cfg c;
+  if (pieces != NP_F16 || cin != 4 * XCK || cout != 32 || !plan_split(H, W, cin, cout, pieces, &c))
+    return 0;
+  if (!(use_pipe() && c.wr && c.NI == 1 && (c.KX == 3 || c.KX == 4))) return 0;
+  if ((size_t)(c.TH + 4) * (W + 2) > 4 * (size_t)c.nwv * 64) return 0;   // XTN x-tile registers
+  return c.lds_pipe + first_lds_extra(c.TH, W) <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int ebsdvae_conv3x3_fwd_split_first(const float* x, const float* st0, const float* w0,
+                                               const float* b0, const void* wpack, const float* bias,
+                                               float* y, float* ypool, float* stat_part, float* st,
+                                               int B, int H, int W, int cin, int cout, int pieces,
+                                               ebsdvae_stream_t stream) {
+  X3Cfg c;
+  EV_REQUIRE(x && st0 && w0 && wpack && (y || ypool) && stat_part && st && B > 0,
+             "conv3x3_fwd_split_first: null pointer or empty batch");
+  EV_REQUIRE(ebsdvae_conv3x3_fwd_split_first_ok(H, W, cin, cout, pieces) &&
+                 plan_split(H, W, cin, cout, pieces, &c),
+             "conv3x3_fwd_split_first: unsupported shape H=%d W=%d cin=%d cout=%d pieces=%d", H, W, cin,
+             cout, pieces);
+  EV_REQUIRE(!ypool || ebsdvae_conv3x3_split_pool_ok(H, W, cin, cout, pieces),
+             "conv3x3_fwd_split_first: pooled output unsupported for H=%d W=%d", H, W);
+  hipStream_t s = (hipStream_t)stream;
+  const bool fused = pipe_owns_images(c, B, H, s);
+  InBwdFuse f;
+  f.ypool = ypool;
+  f.w0 = w0;
+  f.b0 = b0;
+  if (fused) f.st_out = (float2*)st;
+  if (ypool) {
+    if (c.KX == 3)
+      launch_x3_1<NP_F16, 8, 8, 2, 1, 3, ACT_FIRST, FP_POOLOUT, 1, 4>(c, x, st0, wpack, bias, y, stat_part, nullptr, B, H, W, cin, s, f);
+    else
+      launch_x3_1<NP_F16, 8, 8, 2, 1, 4, ACT_FIRST, FP_POOLOUT, 1, 4>(c, x, st0, wpack, bias, y, stat_part, nullptr, B, H, W, cin, s, f);
+  } else {
+    if (c.KX == 3)
+      launch_x3_1<NP_F16, 8, 8, 2, 1, 3, ACT_FIRST, FP_NONE, 1, 4>(c, x, st0, wpack, bias, y, stat_part, nullptr, B, H, W, cin, s, f);
+    else
+      launch_x3_1<NP_F16, 8, 8, 2, 1, 4, ACT_FIRST, FP_NONE, 1, 4>(c, x, st0, wpack, bias, y, stat_part, nullptr, B, H, W, cin, s, f);
+  }
+  if (int rc = evh::check_launch("conv3x3_fwd_split_first")) return rc;
+  if (fused) return 0;
+  const int T = ebsdvae_conv3x3_split_stat_tiles(H, W, cout);
+  return ebsdvae_in_stats_finalize(stat_part, st, B, cout, T, (H * W) / T, stream);
 }

@@ -21,7 +21,21 @@ __version__ = "0.2.0"
 # queue with the main one (the step loses its overlap: 8.55 -> 9.30 ms at B = 256, DESIGN.md
 # section 6).  HIP reads the variable when its runtime initialises, so this takes effect when
 # latice is imported before the first GPU call; a value the user set is kept.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+def _hw_queue_default():
+    import sys
+    torch = sys.modules.get("torch")
+    late = torch is not None and torch.cuda.is_initialized()
+    if late and _os.environ.get("GPU_MAX_HW_QUEUES") is None:
+        import warnings
+        warnings.warn("latice: HIP was initialised before `import latice`, so its default of 4 "
+                      "hardware queues per process is in effect; with an RCCL process group the "
+                      "weight-gradient stream then shares a queue with the main stream (~0.7 ms "
+                      "per step at B = 256). Import latice first, or export GPU_MAX_HW_QUEUES=8.",
+                      RuntimeWarning, stacklevel=3)
+    _os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+
+_hw_queue_default()
 
 
 def _extend_path(pkg_path, *sub):

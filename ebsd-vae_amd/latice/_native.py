@@ -50,6 +50,8 @@ SIGNATURES = {
     "ebsdvae_conv3x3_dgrad_inbwd_split": [P, P, P, P, P, I, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_dgrad_inbwd_f16": [P, P, I, P, P, P, P, I, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_fwd_split_st": [P, P, I, P, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ebsdvae_conv3x3_fwd_split_first_ok": [I, I, I, I, I],
+    "ebsdvae_conv3x3_fwd_split_first": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_dgrad_inbwd_f16_bst": [P, P, I, P, P, P, P, I, P, P, I, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_fwd": [P, P, I, P, P, P, I, I, I, I, I, P],
     "ebsdvae_conv3x3_cout1_dgrad": [P, P, P, I, I, I, I, P],

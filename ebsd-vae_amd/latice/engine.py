@@ -272,8 +272,40 @@ def _record(plan_layers, saved):
 
 
 # ----------------------------------------------------------------------------- helpers
+# EBSDVAE_POISON=1 (debug): every buffer the engine hands to a kernel -- outputs, gradients,
+# statistics / slice partials and scratch -- is NaN-filled when allocated, so a kernel that
+# leaves any element of it unwritten, or a consumer that reads one before its producer wrote
+# it, shows up as a NaN in the results (tests/test_gpu_poison.py).  set_poison() switches it.
+_POISON = os.environ.get("EBSDVAE_POISON", "0") not in ("", "0")
+
+
+def set_poison(on: bool) -> None:
+    global _POISON
+    _POISON = bool(on)
+
+
+def poisoned() -> bool:
+    return _POISON
+
+
+def _scratch(*shape, dtype=torch.float32, device):
+    if _POISON:
+        return torch.full(shape, float("nan"), dtype=dtype, device=device)
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
 def _empty(*shape, like):
-    return torch.empty(shape, dtype=torch.float32, device=like.device)
+    return _scratch(*shape, device=like.device)
+
+
+def _empty_like(t):
+    if _POISON:
+        return torch.full_like(t, float("nan"))
+    return torch.empty_like(t)
+
+
+def _f64(*shape, device):
+    return _scratch(*shape, dtype=torch.float64, device=device)
 
 
 # ----------------------------------------------------------------------------- precision
@@ -434,19 +466,62 @@ def _first_valu(layer: ConvLayer) -> bool:
             and N.call("ebsdvae_conv_first_stat_tiles", layer.H, layer.H) > 0)
 
 
-def _conv_first(x, layer: ConvLayer, w, b, B):
+def _conv_first(x, layer: ConvLayer, w, b, B, write_y=True):
+    """write_y=False: the InstanceNorm statistics only (y None) -- the next conv recomputes y
+    from x (conv_forward_first)."""
     H = layer.H
     T = N.call("ebsdvae_conv_first_stat_tiles", H, H)
-    y = _empty(B, H, H, layer.cout, like=w)
+    y = _empty(B, H, H, layer.cout, like=w) if write_y else None
     part = _empty(B, T, layer.cout, 2, like=w)
     st = _empty(B, layer.cout, 2, like=w)
     tag = f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m{layer.src_mode} valu"
     _launch("conv3x3_fwd", conv_flops(B, H, H, 1, layer.cout), N.call, "ebsdvae_conv_first_fwd",
             N.ptr(x), N.ptr(w), N.ptr(b), N.ptr(y), N.ptr(part), B, H, H, layer.cout, N.stream(),
-            tag=tag, nbytes=4 * (x.numel() + y.numel()))
+            tag=tag + ("" if write_y else " stats"),
+            nbytes=4 * (x.numel() + (B * H * H * layer.cout if write_y else 0)))
     N.call("ebsdvae_in_stats_finalize", N.ptr(part), N.ptr(st), B, layer.cout, T, (H * H) // T,
            N.stream())
-    y.ev_first_valu = True   # in_backward_first may recompute it from x
+    if y is not None:
+        y.ev_first_valu = True   # in_backward_first may recompute it from x
+    return y, st
+
+
+# The second block's forward recomputes the first block's activation from x while it stages its
+# halo (ebsdvae_conv3x3_fwd_split_first): y0 is never read by the forward, and inference never
+# writes it (the first conv runs statistics-only).  Bit-identical to reading y0.
+# EBSDVAE_FIRST_FUSE=0: the first conv writes y0 and the second conv reads it (A/B).
+_FIRST_FUSE = os.environ.get("EBSDVAE_FIRST_FUSE", "1") != "0"
+
+
+def first_fuse_ok(plan: Plan, wp1) -> bool:
+    """encoder.1 can take its input as x + the first conv (split-fp16 pack, 32 channels)."""
+    if not (_FIRST_FUSE and len(plan.enc) > 1 and _first_valu(plan.enc[0])):
+        return False
+    L = plan.enc[1]
+    return bool(wp1 is not None and wp1.pieces == PIECES_F16 and L.src_mode == ACT_NORM and N.call(
+        "ebsdvae_conv3x3_fwd_split_first_ok", L.H, L.H, L.cin, L.cout, wp1.pieces))
+
+
+def conv_forward_first(x, st0, w0, b0, layer: ConvLayer, w, b, B, wp, pool_out, keep_y=True):
+    """conv_forward of the second block with its source lrelu(IN(conv(x, w0) + b0)) recomputed
+    from x (st0: the first block's statistics).  Returns (y, st) or (y, st, ypool) as
+    conv_forward."""
+    H = layer.H
+    y = _empty(B, H, H, layer.cout, like=w) if keep_y or not pool_out else None
+    T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, H, layer.cout)
+    part = _empty(B, T, layer.cout, 2, like=w)
+    st = _empty(B, layer.cout, 2, like=w)
+    ypool = _empty(B, H // 2, H // 2, layer.cout, like=w) if pool_out else None
+    ny = B * H * H * layer.cout
+    nb = 4 * (x.numel() + (ny if y is not None else 0) + (ny // 4 if pool_out else 0))
+    tag = f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m{layer.src_mode} x"
+    _launch("conv3x3_fwd", conv_flops(B, H, H, layer.cin, layer.cout), N.call,
+            "ebsdvae_conv3x3_fwd_split_first", N.ptr(x), N.ptr(st0), N.ptr(w0), N.ptr(b0),
+            N.ptr(wp.t), N.ptr(b), N.ptr(y), N.ptr(ypool), N.ptr(part), N.ptr(st), B, H, H,
+            layer.cin, layer.cout, wp.pieces, N.stream(),
+            tag=tag + (" pool" if pool_out else ""), pieces=wp.pieces, nbytes=nb)
+    if pool_out:
+        return y, st, ypool
     return y, st
 
 
@@ -514,14 +589,14 @@ def in_backward(gnext, pmode, y, st, part=None):
     hin = part is not None
     if part is None:
         T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
-        part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
+        part = _f64(B, T, C, 2, device=y.device)
         N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), pmode, N.ptr(y), N.ptr(st), part.data_ptr(),
                B, H, W, C, s)
     bst = getattr(part, "ev_bst", None)   # finalized by the fused input-gradient conv
     if bst is None:
         bst = _empty(B, C, 2, like=y)
         N.call("ebsdvae_in_bwd_finalize", part.data_ptr(), N.ptr(bst), B, C, part.shape[1], H * W, s)
-    gy = torch.empty_like(y)
+    gy = _empty_like(y)
     if _FWD_PIECES.get(_PRECISION):
         # per-tile max |gy|: the scale of the split-fp16 input-gradient conv that consumes gy
         Tg = N.call("ebsdvae_in_bwd_apply_tiles", B, H, W, C)
@@ -759,7 +834,7 @@ def _flush_reduces(q):
                 N.WgradReduceDesc(N.ptr(wp), N.ptr(bp), N.ptr(dw), N.ptr(db), S_, cin, cout, kind)
                 for wp, bp, S_, cin, cout, kind, dw, db, _ in chunk])
             nbytes = N.call("ebsdvae_wgrad_reduce_batch_work", ctypes.addressof(descs), len(chunk))
-            work = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
+            work = _f64(nbytes // 8, device=dev)
             N.call("ebsdvae_wgrad_reduce_batch", ctypes.addressof(descs), len(chunk),
                    work.data_ptr(), N.stream())
             if side is not None:
@@ -777,7 +852,7 @@ def _reduce_slices(wpart, bpart, S_, cin, cout, kind, dw, db, on_side=False):
         _flush_reduces([e])   # on the side stream, then joined
     else:
         nbytes = N.call("ebsdvae_wgrad_reduce_work", S_, cin, cout)
-        work = torch.empty(nbytes // 8, dtype=torch.float64, device=wpart.device)
+        work = _f64(nbytes // 8, device=wpart.device)
         N.call("ebsdvae_wgrad_reduce", N.ptr(wpart), N.ptr(bpart), S_, N.ptr(dw), N.ptr(db), cin,
                cout, kind, work.data_ptr(), N.stream())
 
@@ -788,13 +863,13 @@ def in_backward_final(g1, w14, y, st, dw14, db14):
     B, H, W, C = y.shape
     T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
     S_ = B * T
-    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
+    part = _f64(B, T, C, 2, device=y.device)
     wpart = _empty(S_, 9, 1, C, like=y)
     bpart = _empty(S_, 1, like=y)
     N.call("ebsdvae_in_bwd_final_reduce", N.ptr(g1), N.ptr(w14), N.ptr(y), N.ptr(st),
            part.data_ptr(), N.ptr(wpart), N.ptr(bpart), B, H, W, C, N.stream())
     bst = _in_bwd_stats(B, C, T, H * W, part, y)
-    gy = torch.empty_like(y)
+    gy = _empty_like(y)
     if _FWD_PIECES.get(_PRECISION):
         # per-tile max |gy|: the scale of the split-fp16 convs that consume gy
         gmax = _empty(B, N.call("ebsdvae_in_bwd_final_tiles", H, W), like=y)
@@ -838,7 +913,7 @@ def network_end(plan: Plan, saved, params, x, g_loss=None, scale: float = 1.0):
     x_hat = _empty(B, 1, H, W, like=y13)
     g1 = _empty(B, H, W, like=y13)
     bce = _empty(B, T, like=y13)
-    part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y13.device)
+    part = _f64(B, T, C, 2, device=y13.device)
     wpart = _empty(B * T, 9, 1, C, like=y13)
     bpart = _empty(B * T, like=y13)
     N.call("ebsdvae_net_end", N.ptr(y13), N.ptr(st13), N.ptr(params["decoder.14.weight"]),
@@ -852,7 +927,7 @@ def in_backward_final_from(end: NetEnd, w14, y, st, dw14, db14):
     """in_backward_final with the reduce pass already done by network_end."""
     B, H, W, C = y.shape
     bst = _in_bwd_stats(B, C, end.tiles, H * W, end.part, y)
-    gy = torch.empty_like(y)
+    gy = _empty_like(y)
     if _FWD_PIECES.get(_PRECISION):
         gmax = _empty(B, N.call("ebsdvae_in_bwd_final_tiles", H, W), like=y)
         N.call("ebsdvae_in_bwd_final_apply_max", N.ptr(end.g1), N.ptr(w14), N.ptr(y), N.ptr(st),
@@ -875,7 +950,7 @@ def in_backward_first(gnext, y, st, x, dw0, db0, part=None, w0=None, b0=None):
     hin = part is not None   # gnext is a fused input gradient's h (see in_backward)
     if part is None:
         T = N.call("ebsdvae_in_bwd_tiles", H, W, C)
-        part = torch.empty(B, T, C, 2, dtype=torch.float64, device=y.device)
+        part = _f64(B, T, C, 2, device=y.device)
         N.call("ebsdvae_in_bwd_reduce", N.ptr(gnext), P_ID, N.ptr(y), N.ptr(st), part.data_ptr(),
                B, H, W, C, N.stream())
     bst = _in_bwd_stats(B, C, part.shape[1], H * W, part, y)
@@ -1002,7 +1077,7 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False, ypool=
         # the finalized statistics (part.ev_bst) for in_backward / in_backward_first
         y_prev, st_prev, pmode = prev
         T = N.call("ebsdvae_conv3x3_split_stat_tiles", H, W, layer.cin)
-        part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
+        part = _f64(B, T, layer.cin, 2, device=gy.device)
         bst = _empty(B, layer.cin, 2, like=gy)
         _launch("conv3x3_fwd", flops, N.call, "ebsdvae_conv3x3_dgrad_inbwd_f16_bst", N.ptr(gy),
                 N.ptr(gmax), gmax.shape[1], N.ptr(wd.t), N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev),
@@ -1023,7 +1098,7 @@ def conv_dgrad(gy, layer: ConvLayer, w, prev=None, wd=None, sum_up=False, ypool=
     y_prev, st_prev, pmode = prev
     T = N.call("ebsdvae_conv3x3_split_stat_tiles" if wd.pieces else "ebsdvae_conv3x3_stat_tiles",
                H, W, layer.cin)
-    part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
+    part = _f64(B, T, layer.cin, 2, device=gy.device)
     args = (N.ptr(gy), N.ptr(wd.t), N.ptr(gin), N.ptr(y_prev), N.ptr(st_prev), pmode,
             part.data_ptr(), B, H, W, layer.cout, layer.cin)
     if wd.pieces:
@@ -1064,7 +1139,7 @@ def conv_dwgrad(gy, layer: ConvLayer, wd, src, sst, src_mode, dw, db):
     T = N.call("ebsdvae_conv3x3_dwgrad_stat_tiles", H, W)
     Hs, Ws = src.shape[1], src.shape[2]
     gin = _empty(B, Hs, Ws, layer.cin, like=gy)
-    part = torch.empty(B, T, layer.cin, 2, dtype=torch.float64, device=gy.device)
+    part = _f64(B, T, layer.cin, 2, device=gy.device)
     wpart = _empty(S_, 9, layer.cout, layer.cin, like=gy)
     bpart = _empty(S_, layer.cout, like=gy)
     tag = f"dwgrad {layer.name:13s} {layer.cout:3d}->{layer.cin:3d} @{H:3d} m{src_mode}"
@@ -1081,7 +1156,7 @@ def conv_dwgrad(gy, layer: ConvLayer, wd, src, sst, src_mode, dw, db):
 def _grad_buf(grads, name, like):
     if grads is not None and name in grads:
         return grads[name]
-    return torch.empty_like(like)
+    return _empty_like(like)
 
 
 # ----------------------------------------------------------------------------- encoder
@@ -1099,6 +1174,7 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True, packs_ready=N
     saved = {}
     src, sst = x, None
     pooled = None   # the previous layer's max-pooled raw output, when it emitted one
+    fuse1 = None    # encoder.1 recomputes the first block from x: (w0, b0, st0)
     for i, L in enumerate(plan.enc):
         w, b = params[L.name + ".weight"], params[L.name + ".bias"]
         if packs_ready is not None and not (i == 0 and _first_valu(L)):
@@ -1108,12 +1184,33 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True, packs_ready=N
         if wp is None and not _first_valu(L):
             wp = pack_weight(w, L, dgrad=False)
         nxt = plan.enc[i + 1] if i + 1 < len(plan.enc) else None
+        if i == 0 and _first_valu(L) and len(plan.enc) > 1:
+            L1 = plan.enc[1]
+            wp1 = _wp(packs, L1.name, 0)
+            if wp1 is None and _FIRST_FUSE:
+                wp1 = pack_weight(params[L1.name + ".weight"], L1, dgrad=False)
+            if first_fuse_ok(plan, wp1):
+                # training keeps y0 for the backward (the first block's pass recomputes it, the
+                # second conv's weight and input gradients read it); inference never writes it
+                y, st = _conv_first(x, L, w, b, B, write_y=train)
+                fuse1 = (w, b, st)
+                if train:
+                    saved[L.name] = (y, st)
+                src, sst = y, st
+                continue
         # producer of a max-pool-fed layer: emit the pooled raw output in the epilogue, so
         # the consumer (and its wgrad) read (H/2)^2 pixels in ACT_NORM mode instead of
         # pooling the full-resolution output while staging
         pool_out = (nxt is not None and nxt.src_mode == ACT_NORM_POOL and L.src_mode == ACT_NORM
                     and pool_out_ok(L, wp))
-        if pooled is not None:
+        if i == 1 and fuse1 is not None:
+            w0, b0, st0 = fuse1
+            if pool_out:
+                y, st, ypool = conv_forward_first(x, st0, w0, b0, L, w, b, B, wp, True,
+                                                  keep_y=train or _EVAL_Y)
+            else:
+                y, st = conv_forward_first(x, st0, w0, b0, L, w, b, B, wp, False)
+        elif pooled is not None:
             y, st = conv_forward(pooled, sst, L, w, b, B, wp=wp, mode=ACT_NORM)
             if train:
                 saved[L.name + ".pool_in"] = pooled
@@ -1243,7 +1340,7 @@ def _heads_work(B, plan: Plan, like):
     if nbytes <= 0:
         raise RuntimeError(f"heads: unsupported shape C={plan.enc_channels} S={plan.enc_side} "
                            f"L={plan.latent_dim}")
-    return torch.empty(nbytes // 4, dtype=torch.float32, device=like.device)
+    return _scratch(nbytes // 4, device=like.device)
 
 
 def heads_forward(plan: Plan, enc, params, eps):
@@ -1282,7 +1379,7 @@ def heads_backward(plan: Plan, g_dec, g_z, g_mu, g_std, flat, std, z, eps, param
         ctx = torch.cuda.stream(side)
     with ctx:
         nbytes = N.call("ebsdvae_heads_wgrad_work", B, F, L)
-        work = torch.empty(nbytes // 4, dtype=torch.float32, device=g_dec.device)
+        work = _scratch(nbytes // 4, device=g_dec.device)
         N.call("ebsdvae_heads_wgrad", N.ptr(flat), N.ptr(z), N.ptr(gs),
                *[N.ptr(out[n]) for n in HEAD_NAMES], N.ptr(work), B, F, L, N.stream())
     if side is not None:
@@ -1385,7 +1482,7 @@ def loss_forward(x_hat, x, z, mu, std, kl_lambda: float):
     # outputs allocated on the current stream (the caller's), written on the side stream and
     # kept alive until the join
     elbo, kl, recon = _empty(B, like=x_hat), _empty(B, like=x_hat), _empty(B, like=x_hat)
-    loss, kl_loss, recon_loss = (torch.empty((), dtype=torch.float32, device=x_hat.device)
+    loss, kl_loss, recon_loss = (_scratch(device=x_hat.device)
                                  for _ in range(3))
     side = _side_stream(x_hat.device) if _DEFER else None
     ctx = contextlib.nullcontext()
@@ -1404,7 +1501,7 @@ def loss_forward_parts(end: NetEnd, z, mu, std, kl_lambda: float, P: int):
     """loss_forward with the BCE sums of network_end (same outputs, same side-stream rule)."""
     B, L = z.shape
     elbo, kl, recon = _empty(B, like=z), _empty(B, like=z), _empty(B, like=z)
-    loss, kl_loss, recon_loss = (torch.empty((), dtype=torch.float32, device=z.device)
+    loss, kl_loss, recon_loss = (_scratch(device=z.device)
                                  for _ in range(3))
     side = _side_stream(z.device) if _DEFER else None
     ctx = contextlib.nullcontext()
@@ -1424,7 +1521,7 @@ def loss_backward(x_hat, x, z, mu, std, kl_lambda: float, g_loss=None, g_kl=None
     logit gradient); g_xhat is then None."""
     if x_hat is None:
         B, L = z.shape
-        g_z, g_mu, g_std = torch.empty_like(z), torch.empty_like(mu), torch.empty_like(std)
+        g_z, g_mu, g_std = _empty_like(z), _empty_like(mu), _empty_like(std)
         N.call("ebsdvae_vae_loss_bwd", None, None, N.ptr(z), N.ptr(mu), N.ptr(std),
                float(kl_lambda), N.ptr(g_loss), N.ptr(g_kl), N.ptr(g_recon), N.ptr(g_elbo),
                float(scale), None, N.ptr(g_z), N.ptr(g_mu), N.ptr(g_std), None, B, P, L, N.stream())
@@ -1435,10 +1532,10 @@ def loss_backward(x_hat, x, z, mu, std, kl_lambda: float, g_loss=None, g_kl=None
     P = x_hat[0].numel()
     L = z.shape[1]
     if out is None:
-        out = (torch.empty_like(x_hat), torch.empty_like(z), torch.empty_like(mu),
-               torch.empty_like(std))
+        out = (_empty_like(x_hat), _empty_like(z), _empty_like(mu),
+               _empty_like(std))
     g_xhat, g_z, g_mu, g_std = out
-    g_x = torch.empty_like(x) if need_gx else None
+    g_x = _empty_like(x) if need_gx else None
     N.call("ebsdvae_vae_loss_bwd", N.ptr(x_hat), N.ptr(x), N.ptr(z), N.ptr(mu), N.ptr(std),
            float(kl_lambda), N.ptr(g_loss), N.ptr(g_kl), N.ptr(g_recon), N.ptr(g_elbo),
            float(scale), N.ptr(g_xhat), N.ptr(g_z), N.ptr(g_mu), N.ptr(g_std), N.ptr(g_x),

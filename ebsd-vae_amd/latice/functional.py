@@ -139,6 +139,29 @@ class VAELossFn(torch.autograd.Function):
         return g_z, g_xhat, g_mu, g_std, g_x, None
 
 
+class KLFn(torch.autograd.Function):
+    """(z, mu, std) -> per-sample Monte-Carlo KL, unscaled (lightning_module.py:94-120):
+    mean_j [log N(z; mu, std) - log N(z; 0, 1)], read directly from the loss kernel's kl_b
+    output at lambda = 1 with an all-zero BCE partial (ebsdvae_vae_loss_fwd_parts), so no
+    reconstruction term is added and subtracted again."""
+
+    @staticmethod
+    def forward(ctx, z, mu, std):
+        z, mu, std = (_f32c(t) for t in (z, mu, std))
+        B = z.shape[0]
+        end = E.NetEnd(None, None, None, None, torch.zeros(B, 1, device=z.device), 1)
+        _, (_, kl, _) = E.loss_forward_parts(end, z, mu, std, 1.0, 1)
+        ctx.save_for_backward(z, mu, std)
+        return kl
+
+    @staticmethod
+    def backward(ctx, g):
+        z, mu, std = ctx.saved_tensors
+        # d kl_b / d(z, mu, std) == d elbo_b / d(z, mu, std) when there is no x_hat
+        _, g_z, g_mu, g_std, _ = E.loss_backward(None, None, z, mu, std, 1.0, g_elbo=_f32c(g), P=1)
+        return g_z, g_mu, g_std
+
+
 class LinearFn(torch.autograd.Function):
     """nn.Linear on the HIP path (direct calls of model.mu / .logvar / .linear2)."""
 

@@ -17,7 +17,7 @@ import torch
 from torch import nn
 from torch.optim import Optimizer
 
-from .functional import VAELossFn
+from .functional import KLFn, VAELossFn
 from .model import VariationalAutoEncoder
 from .optim import FusedAdam
 
@@ -92,13 +92,8 @@ class VAELoss:
         return elbo
 
     def kl_divergence(self, z, mu, std):
-        """Per-sample MC KL (:94-120) (unscaled), via the fused kernel."""
-        B = z.shape[0]
-        # a zero-logit reconstruction against target 0.5 has a constant BCE of log(2)
-        xh = torch.zeros(B, 4, device=z.device, dtype=torch.float32)
-        tgt = torch.full((B, 4), 0.5, device=z.device, dtype=torch.float32)
-        *_, elbo = VAELossFn.apply(z, xh, mu, std, tgt, 1.0)
-        return elbo - math.log(2.0)
+        """Per-sample MC KL (:94-120) (unscaled): the loss kernel's own kl_b at lambda = 1."""
+        return KLFn.apply(z, mu, std)
 
     def compute_loss(self, z, x_hat, mu, std, x) -> dict[str, torch.Tensor]:
         """:122-156 -> {"loss", "kl_loss", "recon_loss", "elbo"}; kl_loss is already x lambda."""

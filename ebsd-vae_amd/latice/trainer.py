@@ -129,6 +129,9 @@ class VAETrainer:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             dist.broadcast(self.flat, src=src, group=group)
         self._eps = None
+        # bench.py (N > 1): events around the gradient exchange's exposed tail
+        self.time_allreduce = False
+        self.allreduce_events = []
         self.graph = None
         self._static = None
         self.packset = E.PackSet(self.plan, self.P)   # params are views of self.flat
@@ -147,6 +150,8 @@ class VAETrainer:
         """fwd + loss + bwd into self.gflat (+ the DP gradient exchange).  Returns the three
         loss scalars (device tensors)."""
         plan, P, G = self.plan, self.P, self.G
+        if E.poisoned():   # debug: every gradient element must be written by this step
+            self.gflat.fill_(float("nan"))
         # one launch packs every conv weight of the step, and the reparameterisation noise is
         # drawn: both on the side stream, beside the first conv (which reads its weight
         # unpacked); the current stream waits for them before the first packed layer
@@ -195,9 +200,27 @@ class VAETrainer:
                 if self._deep_last:
                     hooks[self._deep_last] = lambda: self._start_behind_side(1, x.device)
             E.encoder_backward(plan, g_enc, x, se, P, grads=G, packs=packs, after_wgrad=hooks)
+        ev = None
+        if self.time_allreduce and self.reducer.active:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()   # the backward (both streams, joined above) is done here
         self.reducer.start(len(self.reducer.bounds) - 2)   # the last bucket
         self.reducer.finish()
+        if ev is not None:
+            ev[1].record()   # ... and every bucket's all-reduce here
+            self.allreduce_events.append(ev)
         return loss, kl, rec
+
+    def allreduce_exposed_ms(self):
+        """Mean GPU time per timed step between the end of the backward and the completion of
+        the last all-reduce (the part of the gradient exchange no backward work hides), over
+        the steps run with time_allreduce set; None when no collective ran.  Synchronises."""
+        if not self.allreduce_events:
+            return None
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in self.allreduce_events]
+        self.allreduce_events = []
+        return sum(ms) / len(ms)
 
     def _start_behind_side(self, bucket: int, device):
         """Start a bucket's all-reduce behind everything issued so far on both streams: the

@@ -121,7 +121,8 @@ int ebsdvae_conv3x3_dgrad_inbwd(const float* g, const float* wpack, float* gin,
  * InstanceNorm partials part[b][t][c] = {mean, M2} over row band t of n = H*W/T pixels,
  * T = ebsdvae_conv_first_stat_tiles(H, W) (-1: shape unsupported; W must divide 512), for
  * ebsdvae_in_stats_finalize.  Its arithmetic is the fixed fma chain that
- * ebsdvae_in_bwd_first_apply_wgrad_rc recomputes y with. */
+ * ebsdvae_in_bwd_first_apply_wgrad_rc and ebsdvae_conv3x3_fwd_split_first recompute y with.
+ * y may be NULL: the statistics only (inference, where the next conv recomputes y from x). */
 int ebsdvae_conv_first_stat_tiles(int H, int W);
 int ebsdvae_conv_first_fwd(const float* x, const float* w0, const float* b0, float* y,
                            float* part, int B, int H, int W, int C, ebsdvae_stream_t stream);
@@ -207,6 +208,22 @@ int ebsdvae_conv3x3_fwd_split_st(const float* src, const float* src_stats, int s
                                  const void* wpack, const float* bias, float* y, float* ypool,
                                  float* stat_part, float* st, int B, int H, int W, int cin,
                                  int cout, int pieces, ebsdvae_stream_t stream);
+/* The second conv block's forward (latice/model.py:111, encoder.1) with its input -- the
+ * first block's activation lrelu(IN(y0)), y0 = conv(x, w0) + b0 -- recomputed from x while the
+ * halo is staged, so y0 is never read (inference: never written either):
+ *   x (B,1,H,W), st0 (B, cin) {mean, rstd} of y0 (ebsdvae_conv_first_fwd with y = NULL +
+ *   ebsdvae_in_stats_finalize), w0 (cin,1,3,3), b0 (cin) or NULL;
+ *   the rest as ebsdvae_conv3x3_fwd_split_st with src_mode = ACT_NORM on y0.
+ * Each staged value is the first conv's own fma chain (ebsdvae_conv_first_fwd) followed by the
+ * same normalisation, so y, ypool and st are bit-identical to the two-launch form.  Needs
+ * pieces = EBSDVAE_PIECES_F16 and cin = 32 (the split kernel's resident-weight form):
+ * ebsdvae_conv3x3_fwd_split_first_ok returns 1 for a supported shape, 0 otherwise. */
+int ebsdvae_conv3x3_fwd_split_first_ok(int H, int W, int cin, int cout, int pieces);
+int ebsdvae_conv3x3_fwd_split_first(const float* x, const float* st0, const float* w0,
+                                    const float* b0, const void* wpack, const float* bias,
+                                    float* y, float* ypool, float* stat_part, float* st, int B,
+                                    int H, int W, int cin, int cout, int pieces,
+                                    ebsdvae_stream_t stream);
 int ebsdvae_conv3x3_dgrad_inbwd_f16_bst(const float* g, const float* gmax, int gm_tiles,
                                         const void* wpack, float* gin, const float* y_prev,
                                         const float* st_prev, int pmode, double* part, float* bst,

@@ -91,7 +91,12 @@ def test_nccl_side_stream_allreduce_world1(cuda):
             tr = VAETrainer(m.to(cuda), kl_lambda=5e-6, force_allreduce=force)
             assert tr.reducer.active == force and tr.world == 1
             assert E.side_streams_enabled()
+            tr.time_allreduce = True
             tr.forward_backward(x, eps)
+            exposed = tr.allreduce_exposed_ms()   # bench.py's allreduce_exposed_ms
+            assert (exposed is None) == (not force)
+            if force:
+                assert 0.0 <= exposed < 1e3
             g = tr.gflat.clone()
             tr.optimizer_step()
             torch.cuda.synchronize()
@@ -124,4 +129,5 @@ def test_bench_self_launches_ranks(cuda):
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 16
     assert res["process_group"]["backend"] == "gloo" and res["process_group"]["world_size"] == 2
     assert len(res["rank_ms_per_step"]) == 2 and res["rank_spread_pct"] >= 0
+    assert res["allreduce_exposed_ms"] is not None and res["allreduce_exposed_ms"] >= 0
     assert "gloo grad all-reduce (rehearsal" in res["config"]["workload"]

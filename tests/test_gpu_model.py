@@ -148,3 +148,36 @@ def test_encoder_only_latents_vs_reference(cuda, name, prec):
     assert O.rel_err(h(mu), f["mu"]) < 1e-4
     _, _, mu_full, _ = m(torch.from_numpy(f["x"]).to(cuda), eps=torch.from_numpy(f["eps"]).to(cuda))
     assert torch.allclose(mu, mu_full.detach(), rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-3])
+def test_vae_loss_kl_divergence_and_bce_vs_oracle(cuda, scale):
+    """VAELoss.kl_divergence (lightning_module.py:94-120, per sample, unscaled) and
+    binary_cross_entropy (:79-92) against the float64 oracle (oracle/vae_oracle.py vae_loss at
+    lambda = 1), values and input gradients.  scale = 1e-3 puts mu, z and log std at ~1e-3, so
+    the KL is ~1e-6 -- far below log 2, where a KL taken as (elbo - log 2) keeps no digits."""
+    g = torch.Generator().manual_seed(7)
+    B, L = 64, 16
+    mu = torch.randn(B, L, generator=g, dtype=torch.float64) * scale
+    std = torch.exp(scale * torch.randn(B, L, generator=g, dtype=torch.float64))
+    z = mu + std * scale * torch.randn(B, L, generator=g, dtype=torch.float64)
+    # the oracle sees the fp32-rounded inputs the kernel sees
+    mu_n, std_n, z_n = (t.float().double().numpy() for t in (mu, std, z))
+    kl_ref = (0.5 * z_n ** 2 - 0.5 * ((z_n - mu_n) / std_n) ** 2 - np.log(std_n)).mean(-1)
+    # d kl_b / d(z, mu, std) of the float64 restatement
+    gz_ref = (z_n - (z_n - mu_n) / std_n ** 2) / L
+    gmu_ref = ((z_n - mu_n) / std_n ** 2) / L
+    gstd_ref = ((z_n - mu_n) ** 2 / std_n ** 3 - 1.0 / std_n) / L
+    zz, mm, ss = (t.float().to(cuda).requires_grad_(True) for t in (z, mu, std))
+    kl = VAELoss(kl_lambda=0.5).kl_divergence(zz, mm, ss)
+    kl.sum().backward()
+    torch.cuda.synchronize()
+    assert O.rel_err(h(kl), kl_ref) < 2e-5
+    for t, ref in ((zz, gz_ref), (mm, gmu_ref), (ss, gstd_ref)):
+        assert O.rel_err(h(t.grad), ref) < 1e-5
+    # the BCE half: per-sample mean BCE-with-logits against the oracle's recon term
+    xh = torch.randn(4, 1, 16, 16, generator=g, dtype=torch.float64) * 3
+    x = torch.rand(4, 1, 16, 16, generator=g, dtype=torch.float64)
+    ref = O.vae_loss(xh.numpy(), x.numpy(), z_n[:4], mu_n[:4], std_n[:4], 0.0)["elbo"]
+    bce = VAELoss().binary_cross_entropy(xh.float().to(cuda), x.float().to(cuda))
+    assert O.rel_err(h(bce), ref) < 1e-5
