@@ -366,6 +366,375 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
   }
 }
 
+
+// ------------------------------------------------------------------ MFMA form (round 6)
+// The same outputs with the three 288-MAC-per-pixel contractions on v_mfma_f32_16x16x32_f16
+// (split-fp16 pieces, products a0b0 + a0b1 + a1b0 as in the convs), leaving the VALU only the
+// normalise / LeakyReLU / split, the sigmoid / BCE and the bookkeeping:
+//   (1) tap planes U[q][t] = sum_c a[q][c] w[c][t] of each source row (M = 16 pixels, N = 16
+//       taps of which 9 are live, K = 32 channels): a lane's A fragment is one pixel's 8
+//       channels, exactly as it loads them;
+//   (2) per own row q, with g1 taken at q - d_t:
+//         G[c][t] = sum_q a[q][c] g1[q - d_t]            (the final conv's weight gradient)
+//         P[c][t] = sum_q [a[q][c] > 0] g1[q - d_t]      (indicator: exact in fp16)
+//       (M = 16 channels, N = 16 taps, K = 32 pixels, the a / indicator fragments read from a
+//       per-wave pixel-major LDS image with ds_read_b64_tr_b16, the g1 fragments from three
+//       column-shifted copies of the g1 row);
+//   and the block's InstanceNorm-backward reduce follows from them by two identities: with
+//   ga[q][c] = sum_t w[c][t] g1[q - d_t] (the final conv's input gradient) and a = lrelu(xhat),
+//       s2[c] = sum_q ga m xhat = sum_q ga a           = sum_t w[c][t] G[c][t]
+//       s1[c] = sum_q ga m      = sum_t w[c][t] (slope S[t] + (1 - slope) P[c][t]),
+//   m = lrelu'(xhat) in {1, slope} and S[t] = sum_q g1[q - d_t] (channel-free, on the VALU).
+// Every quantity is restricted to the band's own rows q, as in net_end_kernel, so the band
+// partials sum to the image's.  g1 is scaled by 2^kg (|g1| <= |cr| = the loss gradient scale,
+// known at launch) and the weights by 2^kw (their block-wide maximum) into fp16's range; both
+// are undone exactly.
+template <int W> constexpr int nm_urs() { return W + 8; }            // plane row: col c at c + 4
+template <int W> constexpr size_t nm_lds() {
+  return (size_t)NE_RING * 9 * nm_urs<W>() * 4        // tap planes
+         + (size_t)NE_RING * 3 * 2 * W * 2              // g1 rows: [slot][kw][piece][W] fp16
+         + (size_t)(W / 32) * 3 * 32 * 96;              // per-wave a0 / a1 / indicator images
+}
+constexpr int NM_IMG = 32 * 96;   // one per-wave image: 32 pixel rows of 32 channels (64 B + 32 pad)
+
+EV_DEVINL f16x8 nm_pack(const unsigned (&v)[4]) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(f16x8, u4{v[0], v[1], v[2], v[3]});
+}
+EV_DEVINL f16x8 nm_tr(const char* r0, const char* r1) {
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  typedef __attribute__((address_space(3))) s16x4* lds_s16x4_ptr;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(r0));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(r1));
+  const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(f16x8, v);
+}
+EV_DEVINL f32x4 nm_mfma(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+template <int W>
+__global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
+    const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
+    const float* __restrict__ b14, const float* __restrict__ xt, const float* __restrict__ g_loss,
+    float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
+    double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
+  constexpr int C = NE_C, TH = NE_TH, NWAVE = W / 32, NTH = 64 * NWAVE;
+  constexpr int URS = nm_urs<W>(), UROWS = 9 * URS;
+  extern __shared__ __attribute__((aligned(16))) float ne_sm[];
+  float* uring = ne_sm;                                                   // [4][9][URS]
+  _Float16* gring = reinterpret_cast<_Float16*>(ne_sm + NE_RING * UROWS);  // [4][3][2][W]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, gq = lane >> 4;
+  char* img = reinterpret_cast<char*>(gring + NE_RING * 6 * W) + wave * 3 * NM_IMG;
+  const int tile = blockIdx.x, b = blockIdx.y, T = gridDim.x;
+  const int r0 = tile * TH;
+  const size_t HW = (size_t)H * W;
+  const int px_w = wave * 32;   // the wave's 32 pixel columns
+
+  // normalisation of this lane's 8 channels 8 gq .. 8 gq + 7, as channel pairs (net_end_kernel's)
+  pkf2 fsr[4], fsb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float2 f0 = norm_fs(st[(size_t)b * C + 8 * gq + 2 * k]);
+    const float2 f1 = norm_fs(st[(size_t)b * C + 8 * gq + 2 * k + 1]);
+    fsr[k] = pk2(f0.x, f1.x);
+    fsb[k] = pk2(f0.y, f1.y);
+  }
+  // (1)'s B fragment: w14[c = 8 gq + j][t = l16] (t >= 9: 0), scaled by 2^kw, two fp16 pieces
+  f16x8 wb0, wb1;
+  int kw_;
+  {
+    float wv[8], m = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wv[j] = l16 < 9 ? w14[(8 * gq + j) * 9 + l16] : 0.f;
+      m = fmaxf(m, fabsf(wv[j]));
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    kw_ = f16_shift_of(m);
+    const float s = ldexpf(1.f, kw_);
+    unsigned h[4], lo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) split_f16x2_scaled(wv[2 * p], wv[2 * p + 1], s, h[p], lo[p]);
+    wb0 = nm_pack(h);
+    wb1 = nm_pack(lo);
+  }
+  const float uscale = ldexpf(1.f, -kw_);
+  const float bias = b14 ? b14[0] : 0.f;
+  const float cr = gscale * (g_loss ? *g_loss : 1.f);   // g_loss * scale / (B * P)
+  const int kg = f16_shift_of(fabsf(cr));               // |g1| <= |cr|
+  const float gsc = ldexpf(1.f, kg);
+
+  // zero columns of the tap planes (col -1 and W) and the two never-written g1 copy entries
+  for (int i = tid; i < NE_RING * 9 * 2; i += NTH) {
+    const int rw = i >> 1;
+    uring[rw * URS + ((i & 1) ? W + 4 : 3)] = 0.f;
+  }
+  if (tid < NE_RING * 2 * 2) {   // [slot][piece][copy 0 at W-1 | copy 2 at 0]
+    const int sl = tid >> 2, pc = (tid >> 1) & 1, which = tid & 1;
+    gring[((sl * 3 + (which ? 2 : 0)) * 2 + pc) * W + (which ? 0 : W - 1)] = (_Float16)0.f;
+  }
+
+  const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + (size_t)b * HW * C), 0,
+                                                    (int)(HW * C * 4), 0x00020000);
+  auto load_row = [&](int q, float4 (&d)[2][2]) EV_LAMBDA_INLINE {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        d[g][h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  ry, ((q * W + px_w + g * 16 + l16) * C + 8 * gq + 4 * h) * 4, 0, 0));
+  };
+  const bool xlane = lane < 32;   // the lanes that run the per-pixel part (pixel px_w + lane)
+  auto load_tgt = [&](int r, float& d) EV_LAMBDA_INLINE {
+    d = (r >= 0 && r < H && xlane) ? xt[(size_t)b * HW + (size_t)r * W + px_w + lane] : 0.f;
+  };
+
+  f32x4 G[2], P[2];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) G[mb] = P[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float S[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) S[t] = 0.f;
+  float bsum = 0.f, bce = 0.f;
+  // a0 / a1 / indicator fragments of source rows q - 1 and q - 2 (rows of (2) two steps later)
+  f16x8 pa[3][2], pb[3][2];   // [tensor][group]; pa = row q - 1, pb = row q - 2
+#pragma unroll
+  for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) pa[t3][g] = pb[t3][g] = f16x8{};
+  float4 ybuf[2][2][2];
+  float tbuf[2];
+  load_row(r0 - 2, ybuf[0]);
+  load_row(r0 - 1, ybuf[1]);
+  load_tgt(r0 - 3, tbuf[0]);
+  load_tgt(r0 - 2, tbuf[1]);
+  // (2)'s g1 fragment geometry: tap t = l16 (t >= 9: zero), 4 + 4 pixels of the wave's 32
+  const int tkh = l16 < 9 ? l16 / 3 : 0, tkw = l16 < 9 ? l16 % 3 : 0;
+  const bool tlive = l16 < 9;
+  __syncthreads();
+
+  auto step = [&](int i, float4 (&ycur)[2][2], float& tcur, f16x8 (&pn)[3][2]) EV_LAMBDA_INLINE {
+    const int q = r0 - 2 + i;
+    // ---- (1) a of source row q: registers (pn), tap planes into ring slot i & 3
+    if (q >= 0 && q < H) {   // block-uniform
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        float a[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 v = ycur[g][h];
+          const pkf2 u0 = pkfma(pk2(v.x, v.y), fsr[2 * h], fsb[2 * h]);
+          const pkf2 u1 = pkfma(pk2(v.z, v.w), fsr[2 * h + 1], fsb[2 * h + 1]);
+          const pkf2 k0 = u0 * pk2(kSlope, kSlope), k1 = u1 * pk2(kSlope, kSlope);
+          a[4 * h + 0] = fmaxf(u0.x, k0.x); a[4 * h + 1] = fmaxf(u0.y, k0.y);
+          a[4 * h + 2] = fmaxf(u1.x, k1.x); a[4 * h + 3] = fmaxf(u1.y, k1.y);
+        }
+        unsigned h0[4], h1[4], ind[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          split_f16x2(a[2 * p], a[2 * p + 1], h0[p], h1[p]);
+          ind[p] = (a[2 * p] > 0.f ? 0x3C00u : 0u) | (a[2 * p + 1] > 0.f ? 0x3C000000u : 0u);
+        }
+        pn[0][g] = nm_pack(h0);
+        pn[1][g] = nm_pack(h1);
+        pn[2][g] = nm_pack(ind);
+      }
+    } else {
+#pragma unroll
+      for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) pn[t3][g] = f16x8{};
+    }
+    load_row(q + 2, ycur);   // prefetch into the registers just consumed
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
+      u = nm_mfma(pn[1][g], wb0, u);
+      u = nm_mfma(pn[0][g], wb1, u);
+      u = nm_mfma(pn[0][g], wb0, u);
+      if (tlive)   // C/D: rows (pixels) 4 gq .. 4 gq + 3 of the group, column l16 = tap
+        *reinterpret_cast<float4*>(uring + (i & 3) * UROWS + l16 * URS + 4 + px_w + g * 16 + 4 * gq) =
+            make_float4(u[0] * uscale, u[1] * uscale, u[2] * uscale, u[3] * uscale);
+    }
+    __syncthreads();
+    // ---- x_hat, g1 and BCE of row q - 1 from the planes of rows q - 2 .. q
+    if (i >= 2) {
+      const int r = q - 1;
+      const bool inrow = r >= 0 && r < H, own = r >= r0 && r < r0 + TH;
+      if (xlane) {
+        const int w = px_w + lane;
+        float xh = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const float* u = uring + ((i - 2 + kh) & 3) * UROWS + 4 + w - 1;
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) xh += u[(kh * 3 + kw) * URS + kw];
+        }
+        xh += bias;
+        float g = 0.f;
+        if (inrow) {
+          const float e = expf(-fabsf(xh));
+          g = cr * (ne_sigmoid_e(xh, e) - tcur);
+          if (own) {
+            x_hat[(size_t)b * HW + (size_t)r * W + w] = xh;
+            g1out[(size_t)b * HW + (size_t)r * W + w] = g;
+            bce += ne_bce_e(xh, tcur, e);
+            bsum += g;
+          }
+        }
+        // S[t] = sum over own rows q of g1[q - d_t]: row r feeds tap row kh when
+        // r in [r0 + 1 - kh, r0 + TH + 1 - kh), column w feeds kw unless the shifted
+        // column falls outside the image (w = 0 for kw = 0, w = W - 1 for kw = 2)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+          if (r >= r0 + 1 - kh && r < r0 + TH + 1 - kh) {
+            S[3 * kh + 1] += g;
+            if (w != 0) S[3 * kh] += g;
+            if (w != W - 1) S[3 * kh + 2] += g;
+          }
+        // g1 * 2^kg as two fp16 pieces into the three column-shifted copies of ring slot r & 3:
+        // copy kw holds g1[x + 1 - kw] at x
+        const float gs = g * gsc;
+        const _Float16 q0 = (_Float16)gs;
+        const _Float16 q1 = (_Float16)(gs - (float)q0);
+        _Float16* gr = gring + (size_t)(r & 3) * 6 * W;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int x = w - 1 + kw;
+          if (x >= 0 && x < W) {
+            gr[(kw * 2 + 0) * W + x] = q0;
+            gr[(kw * 2 + 1) * W + x] = q1;
+          }
+        }
+      }
+    }
+    load_tgt(q + 1, tcur);   // x_hat row q + 1 is computed at step i + 2
+    __syncthreads();
+    // ---- (2) G and P of own row q - 2 (its fragments in pb)
+    if (i >= 4) {
+      const int qo = q - 2;
+      // the row's a0 / a1 / indicator as pixel-major images (this wave's 32 pixels)
+#pragma unroll
+      for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          *reinterpret_cast<f16x8*>(img + t3 * NM_IMG + (g * 16 + l16) * 96 + 16 * gq) = pb[t3][g];
+      __builtin_amdgcn_sched_barrier(0);
+      // g1 fragment: tap t = l16 at pixels 4 gq + j and 16 + 4 gq + j (the transposed reads'
+      // K order), row qo - kh + 1
+      const _Float16* gr = gring + (size_t)((qo - tkh + 1) & 3) * 6 * W + px_w + 4 * gq;
+      typedef short s16x4 __attribute__((ext_vector_type(4)));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      f16x8 gb[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const _Float16* gp = gr + (tkw * 2 + pc) * W;
+        const s16x4 lo = *reinterpret_cast<const s16x4*>(gp);
+        const s16x4 hi = *reinterpret_cast<const s16x4*>(gp + 16);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (!tlive) v = s16x8{};
+        gb[pc] = __builtin_bit_cast(f16x8, v);
+      }
+      const int p4 = l16 & 3, qr = l16 >> 2;
+      const int px0 = 4 * gq + qr, px1 = px0 + 16;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        const int col = (16 * mb + 4 * p4) * 2;
+        const f16x8 a0 = nm_tr(img + px0 * 96 + col, img + px1 * 96 + col);
+        const f16x8 a1 = nm_tr(img + NM_IMG + px0 * 96 + col, img + NM_IMG + px1 * 96 + col);
+        const f16x8 ai = nm_tr(img + 2 * NM_IMG + px0 * 96 + col, img + 2 * NM_IMG + px1 * 96 + col);
+        G[mb] = nm_mfma(a1, gb[0], G[mb]);
+        G[mb] = nm_mfma(a0, gb[1], G[mb]);
+        G[mb] = nm_mfma(a0, gb[0], G[mb]);
+        P[mb] = nm_mfma(ai, gb[1], P[mb]);
+        P[mb] = nm_mfma(ai, gb[0], P[mb]);
+      }
+      (void)qo;
+    }
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) { pb[t3][g] = pa[t3][g]; pa[t3][g] = pn[t3][g]; }
+  };
+  f16x8 pn[3][2];
+#pragma unroll 1
+  for (int i = 0; i < TH + 4; i += 2) {
+    step(i, ybuf[0], tbuf[0], pn);
+    step(i + 1, ybuf[1], tbuf[1], pn);
+  }
+  __syncthreads();
+  // ---- band partials, fixed order
+  // G / P: C/D of wave w, M block mb: channel 16 mb + 4 gq + k (k = 0..3), tap l16
+  float* red = ne_sm;   // [NWAVE][2 (G, P)][32 c][16 t]
+  if (tlive) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = 16 * mb + 4 * gq + k;
+        red[((wave * 2 + 0) * 32 + c) * 16 + l16] = G[mb][k];
+        red[((wave * 2 + 1) * 32 + c) * 16 + l16] = P[mb][k];
+      }
+  }
+  // S, bsum, bce: the 32 pixel lanes by a shuffle tree, then the waves
+  float* sred = ne_sm + NWAVE * 2 * 32 * 16;   // [NWAVE][12]
+  {
+    float v[11];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) v[t] = S[t];
+    v[9] = bsum;
+    v[10] = bce;
+#pragma unroll
+    for (int e = 0; e < 11; ++e) {
+      float x = xlane ? v[e] : 0.f;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) x += __shfl_xor(x, o, 64);
+      if (lane == 0) sred[wave * 12 + e] = x;
+    }
+  }
+  __syncthreads();
+  const int slice = b * T + tile;
+  if (tid < C) {   // channel c = tid
+    const int c = tid;
+    double Sd[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float s = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < NWAVE; ++wv) s += sred[wv * 12 + t];
+      Sd[t] = (double)s;
+    }
+    const double ig = 1.0 / (double)gsc;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float gt = 0.f, pt = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < NWAVE; ++wv) {
+        gt += red[((wv * 2 + 0) * 32 + c) * 16 + t];
+        pt += red[((wv * 2 + 1) * 32 + c) * 16 + t];
+      }
+      const float gw = (float)((double)gt * ig);
+      wpart[((size_t)slice * 9 + t) * 32 + c] = gw;
+      const double wct = (double)w14[c * 9 + t];
+      s2 += wct * (double)gw;
+      s1 += wct * ((double)kSlope * Sd[t] + (1.0 - (double)kSlope) * (double)pt * ig);
+    }
+    part[(size_t)slice * C + c] = make_double2(s1, s2);
+  }
+  if (tid == 0) {
+    float bs = 0.f, es = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < NWAVE; ++wv) { bs += sred[wv * 12 + 9]; es += sred[wv * 12 + 10]; }
+    bpart[slice] = bs;
+    bce_part[slice] = es;
+  }
+}
+
 }  // namespace ev
 
 using namespace ev;
@@ -374,13 +743,13 @@ extern "C" int ebsdvae_net_end_tiles(int H, int W) {
   return ((W == 128 || W == 256) && ev_dim_ok(H) && H % NE_TH == 0) ? H / NE_TH : -1;
 }
 
-template <int W>
+template <int W, bool MF>
 static void net_end_launch(dim3 grid, hipStream_t st, const float* y13, const float* st13,
                            const float* w14, const float* b14, const float* x, const float* g_loss,
                            float gscale, float* x_hat, float* g1, float* bce_part, double* part,
                            float* wpart, float* bpart, int H) {
-  auto k = net_end_kernel<W>;
-  constexpr size_t lds = ne_lds_u<W>();
+  auto k = MF ? net_end_mfma_kernel<W> : net_end_kernel<W>;
+  constexpr size_t lds = MF ? nm_lds<W>() : ne_lds_u<W>();
   static bool once = false;
   if (!once) {
     (void)hipFuncSetAttribute((const void*)(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -391,10 +760,11 @@ static void net_end_launch(dim3 grid, hipStream_t st, const float* y13, const fl
                      (double2*)part, wpart, bpart, H);
 }
 
-extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float* w14, const float* b14,
-                               const float* x, const float* g_loss, float scale, float* x_hat,
-                               float* g1, float* bce_part, double* part, float* wpart, float* bpart,
-                               int B, int H, int W, int C, ebsdvae_stream_t stream) {
+template <bool MF>
+static int net_end_entry(const float* y13, const float* st13, const float* w14, const float* b14,
+                         const float* x, const float* g_loss, float scale, float* x_hat,
+                         float* g1, float* bce_part, double* part, float* wpart, float* bpart,
+                         int B, int H, int W, int C, ebsdvae_stream_t stream) {
   EV_REQUIRE(y13 && st13 && w14 && x && x_hat && g1 && bce_part && part && wpart && bpart && B > 0,
              "net_end: null pointer");
   EV_REQUIRE(C == NE_C && ebsdvae_net_end_tiles(H, W) > 0,
@@ -402,10 +772,26 @@ extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float*
   const int T = ebsdvae_net_end_tiles(H, W);
   const float gscale = scale / ((float)B * (float)(H * W));
   if (W == 128)
-    net_end_launch<128>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
-                        g1, bce_part, part, wpart, bpart, H);
+    net_end_launch<128, MF>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale,
+                            x_hat, g1, bce_part, part, wpart, bpart, H);
   else
-    net_end_launch<256>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, x_hat,
-                        g1, bce_part, part, wpart, bpart, H);
+    net_end_launch<256, MF>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale,
+                            x_hat, g1, bce_part, part, wpart, bpart, H);
   return evh::check_launch("net_end");
+}
+
+// the MFMA form (default) and the round-5 VALU form (A/B, EBSDVAE_NET_END_MFMA=0 in the engine)
+extern "C" int ebsdvae_net_end(const float* y13, const float* st13, const float* w14, const float* b14,
+                               const float* x, const float* g_loss, float scale, float* x_hat,
+                               float* g1, float* bce_part, double* part, float* wpart, float* bpart,
+                               int B, int H, int W, int C, ebsdvae_stream_t stream) {
+  return net_end_entry<true>(y13, st13, w14, b14, x, g_loss, scale, x_hat, g1, bce_part, part, wpart,
+                             bpart, B, H, W, C, stream);
+}
+extern "C" int ebsdvae_net_end_valu(const float* y13, const float* st13, const float* w14,
+                                    const float* b14, const float* x, const float* g_loss, float scale,
+                                    float* x_hat, float* g1, float* bce_part, double* part, float* wpart,
+                                    float* bpart, int B, int H, int W, int C, ebsdvae_stream_t stream) {
+  return net_end_entry<false>(y13, st13, w14, b14, x, g_loss, scale, x_hat, g1, bce_part, part, wpart,
+                              bpart, B, H, W, C, stream);
 }

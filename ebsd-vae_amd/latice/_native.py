@@ -98,6 +98,7 @@ SIGNATURES = {
     "ebsdvae_vae_loss_fwd_parts": [P, I, P, P, P, F, P, P, P, P, P, P, I, I, I, P],
     "ebsdvae_net_end_tiles": [I, I],
     "ebsdvae_net_end": [P, P, P, P, P, P, F, P, P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_net_end_valu": [P, P, P, P, P, P, F, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_adam": [P, P, P, P, P, P, I64, F, F, F, F, F, I, P],
     "ebsdvae_l2_normalize_rows": [P, P, I64, I, P],
     "ebsdvae_cosine_topk_work": [I64, I, I, I],
@@ -114,7 +115,7 @@ QUERIES = {"ebsdvae_version", "ebsdvae_conv_first_stat_tiles", "ebsdvae_conv3x3_
            "ebsdvae_wgrad_reduce_batch_work", "ebsdvae_cosine_topk_work",
            "ebsdvae_in_bwd_tiles", "ebsdvae_in_bwd_apply_tiles", "ebsdvae_in_bwd_final_tiles", "ebsdvae_wgrad_reduce_work", "ebsdvae_heads_wgrad_work", "ebsdvae_heads_work",
            "ebsdvae_conv3x3_split_supported", "ebsdvae_conv3x3_split_stat_tiles",
-           "ebsdvae_conv3x3_split_pool_ok",
+           "ebsdvae_conv3x3_split_pool_ok", "ebsdvae_conv3x3_fwd_split_first_ok",
            "ebsdvae_pack_split_bytes", "ebsdvae_conv3x3_wgrad_split_slices", "ebsdvae_net_end_tiles",
            "ebsdvae_conv3x3_dwgrad_slices", "ebsdvae_conv3x3_dwgrad_stat_tiles"}
 

@@ -488,14 +488,20 @@ def _conv_first(x, layer: ConvLayer, w, b, B, write_y=True):
 
 # The second block's forward recomputes the first block's activation from x while it stages its
 # halo (ebsdvae_conv3x3_fwd_split_first): y0 is never read by the forward, and inference never
-# writes it (the first conv runs statistics-only).  Bit-identical to reading y0.
-# EBSDVAE_FIRST_FUSE=0: the first conv writes y0 and the second conv reads it (A/B).
-_FIRST_FUSE = os.environ.get("EBSDVAE_FIRST_FUSE", "1") != "0"
+# writes it (the first conv runs statistics-only).  Bit-identical to reading y0.  Measured
+# (round 6): the staging's extra 36 FMAs per item cost the conv more than
+# the y0 reads it saves (encoder.1 fwd 336 -> 355 us at B = 256), so it pays only where the
+# first conv's 2 GB y0 write goes away too -- inference (c4).  Training keeps y0 (its backward
+# reads it) and the two-launch form.
+# EBSDVAE_FIRST_FUSE: "eval" (default) inference only, "1" also training, "0" never (A/B).
+_FIRST_FUSE = os.environ.get("EBSDVAE_FIRST_FUSE", "eval")
+if _FIRST_FUSE not in ("0", "1", "eval"):
+    raise ValueError("EBSDVAE_FIRST_FUSE must be 0, 1 or eval")
 
 
 def first_fuse_ok(plan: Plan, wp1) -> bool:
     """encoder.1 can take its input as x + the first conv (split-fp16 pack, 32 channels)."""
-    if not (_FIRST_FUSE and len(plan.enc) > 1 and _first_valu(plan.enc[0])):
+    if not (_FIRST_FUSE != "0" and len(plan.enc) > 1 and _first_valu(plan.enc[0])):
         return False
     L = plan.enc[1]
     return bool(wp1 is not None and wp1.pieces == PIECES_F16 and L.src_mode == ACT_NORM and N.call(
@@ -888,6 +894,8 @@ def in_backward_final(g1, w14, y, st, dw14, db14):
 # the last block's InstanceNorm-backward reduce + the final conv's gradient slices in one pass
 # over y13 (the training step; EBSDVAE_NET_END=0 keeps the separate kernels for A/B timing).
 _NET_END = os.environ.get("EBSDVAE_NET_END", "1") != "0"
+# its contractions on the split-fp16 MFMA (round 6); EBSDVAE_NET_END_MFMA=0: the VALU form (A/B)
+_NET_END_MFMA = os.environ.get("EBSDVAE_NET_END_MFMA", "1") != "0"
 
 
 @dataclass
@@ -916,7 +924,7 @@ def network_end(plan: Plan, saved, params, x, g_loss=None, scale: float = 1.0):
     part = _f64(B, T, C, 2, device=y13.device)
     wpart = _empty(B * T, 9, 1, C, like=y13)
     bpart = _empty(B * T, like=y13)
-    N.call("ebsdvae_net_end", N.ptr(y13), N.ptr(st13), N.ptr(params["decoder.14.weight"]),
+    N.call("ebsdvae_net_end" if _NET_END_MFMA else "ebsdvae_net_end_valu", N.ptr(y13), N.ptr(st13), N.ptr(params["decoder.14.weight"]),
            N.ptr(params["decoder.14.bias"]), N.ptr(x), N.ptr(g_loss), float(scale), N.ptr(x_hat),
            N.ptr(g1), N.ptr(bce), part.data_ptr(), N.ptr(wpart), N.ptr(bpart), B, H, W, C,
            N.stream())
@@ -1184,10 +1192,11 @@ def encoder_forward(plan: Plan, x, params, packs=None, train=True, packs_ready=N
         if wp is None and not _first_valu(L):
             wp = pack_weight(w, L, dgrad=False)
         nxt = plan.enc[i + 1] if i + 1 < len(plan.enc) else None
-        if i == 0 and _first_valu(L) and len(plan.enc) > 1:
+        if i == 0 and _first_valu(L) and len(plan.enc) > 1 and \
+                (_FIRST_FUSE == "1" or (_FIRST_FUSE == "eval" and not train)):
             L1 = plan.enc[1]
             wp1 = _wp(packs, L1.name, 0)
-            if wp1 is None and _FIRST_FUSE:
+            if wp1 is None:
                 wp1 = pack_weight(params[L1.name + ".weight"], L1, dgrad=False)
             if first_fuse_ok(plan, wp1):
                 # training keeps y0 for the backward (the first block's pass recomputes it, the

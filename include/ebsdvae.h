@@ -457,7 +457,7 @@ int ebsdvae_vae_loss_fwd_parts(const float* bce_part, int tiles, const float* z,
 
 /* ---- network end of the training step (latice/model.py:147-148 + lightning_module.py:79-92) --
  * One pass over the last block's pre-norm output y13 (B, H, W, C) NHWC with its statistics
- * st13 {mean, rstd} (B, C), for C == 32, W == 128, H % 16 == 0:
+ * st13 {mean, rstd} (B, C), for C == 32, W == 128 or 256, H % 32 == 0:
  *   x_hat (B, 1, H, W) = Conv2d(32, 1)(lrelu(IN(y13))) with w14 (1, 32, 3, 3), b14 (1) or NULL;
  *   g1 (B, H, W) = g_loss * scale / (B * H * W) * (sigmoid(x_hat) - x), the gradient of the
  *     mean-BCE part of the loss w.r.t. the logits (g_loss a device scalar, NULL = 1);
@@ -469,9 +469,16 @@ int ebsdvae_vae_loss_fwd_parts(const float* bce_part, int tiles, const float* z,
  *     ebsdvae_wgrad_reduce (cin C, cout 1, kind 0).
  * T = ebsdvae_net_end_tiles(H, W) (-1: shape unsupported).  Replaces ebsdvae_conv3x3_cout1_fwd,
  * the BCE part of ebsdvae_vae_loss_fwd / _bwd and ebsdvae_in_bwd_final_reduce, which read y13
- * once each. */
+ * once each.  The three contractions run on the split-fp16 MFMA (f16x3 products); the reduce
+ * sums come from the weight-gradient contraction and an indicator contraction
+ * (s2 = sum_t w G, s1 = sum_t w (slope S + (1 - slope) P), net_end.hip).
+ * ebsdvae_net_end_valu: the same outputs from the fp32 VALU form (round 5; A/B). */
 int ebsdvae_net_end_tiles(int H, int W);
 int ebsdvae_net_end(const float* y13, const float* st13, const float* w14, const float* b14,
+                    const float* x, const float* g_loss, float scale, float* x_hat, float* g1,
+                    float* bce_part, double* part, float* wpart, float* bpart, int B, int H, int W,
+                    int C, ebsdvae_stream_t stream);
+int ebsdvae_net_end_valu(const float* y13, const float* st13, const float* w14, const float* b14,
                     const float* x, const float* g_loss, float scale, float* x_hat, float* g1,
                     float* bce_part, double* part, float* wpart, float* bpart, int B, int H, int W,
                     int C, ebsdvae_stream_t stream);

@@ -101,3 +101,15 @@ def test_host_asan_driver():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "AddressSanitizer" not in r.stderr, (r.stdout + r.stderr)[-4000:]
     assert "abi_asan: ok" in r.stdout
+
+
+def test_query_entry_points_are_registered_as_queries():
+    """Size / support queries return their value instead of a status: every one the signature
+    table lists must be in _native.QUERIES, or N.call would raise on its (nonzero) answer."""
+    from latice import _native as N
+    suffixes = ("_ok", "_tiles", "_slices", "_bytes", "_work", "_supported", "_version")
+    queries = {n for n in N.SIGNATURES if n.endswith(suffixes)}
+    assert queries <= N.QUERIES, sorted(queries - N.QUERIES)
+    # and they answer on a CPU-only host (no device call behind them)
+    assert N.call("ebsdvae_conv3x3_fwd_split_first_ok", 128, 128, 32, 32, N.PIECES_F16
+                  if hasattr(N, "PIECES_F16") else 16) == 1

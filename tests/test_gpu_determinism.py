@@ -34,13 +34,19 @@ def _trainer(name, device, copies):
 
 
 def _repeat_steps(m, x, eps, kl):
+    """REPEATS steps in poison mode (engine.set_poison): every buffer the step allocates is
+    NaN-filled first, so a read that races its producer -- on either stream -- returns NaN,
+    not the nearly identical value an earlier step left in the allocator's block."""
     tr = VAETrainer(m, kl_lambda=kl)
     outs = []
-    for _ in range(REPEATS):
-        tr.gflat.fill_(float("nan"))   # a gradient the step failed to write shows as a difference
-        loss, k, r = tr.forward_backward(x, eps)
-        torch.cuda.synchronize()
-        outs.append((torch.stack([loss, k, r]).cpu(), tr.gflat.cpu()))
+    E.set_poison(True)
+    try:
+        for _ in range(REPEATS):
+            loss, k, r = tr.forward_backward(x, eps)   # (poison also NaN-fills tr.gflat first)
+            torch.cuda.synchronize()
+            outs.append((torch.stack([loss, k, r]).cpu(), tr.gflat.cpu()))
+    finally:
+        E.set_poison(False)
     return tr, outs
 
 
@@ -53,7 +59,9 @@ def test_repeated_steps_are_bitwise_equal(cuda, prec, name, copies):
     with E.precision(prec):
         tr, outs = _repeat_steps(m, x, eps, kl)
     l0, g0 = outs[0]
-    assert torch.isfinite(g0).all(), "a gradient entry was never written"
+    for li, gi in outs:
+        assert torch.isfinite(li).all() and torch.isfinite(gi).all(), \
+            "a NaN from a poisoned buffer: an entry never written, or read before it was"
     bad = []
     for i, (li, gi) in enumerate(outs[1:], 1):
         if not torch.equal(li, l0):

@@ -2,7 +2,8 @@
 (ebsdvae_conv3x3_fwd_split_first, engine.conv_forward_first): every staged value is the first
 conv's own fma chain (ebsdvae_conv_first_fwd) followed by the same normalisation, so the
 block's outputs must be BITWISE those of the two-launch form that writes y0 and reads it back
-(EBSDVAE_FIRST_FUSE=0).  Checked at the bench shapes -- c2 (128^2, B = 256: whole-image
+(EBSDVAE_FIRST_FUSE=0).  The default uses it in inference only ("eval": the first conv then
+writes no y0 at all); "1" also in training.  Checked at the bench shapes -- c2 (128^2, B = 256: whole-image
 persistent blocks, in-kernel finalize), c4's encoder-only inference (no y0 at all) and c5
 (256^2, four staged items per thread) -- and on a ragged batch (B = 5: the standalone finalize).
 """
@@ -24,7 +25,7 @@ def _model(cuda, S, L):
 
 
 def _encode(m, x, train, fuse, monkeypatch):
-    monkeypatch.setattr(E, "_FIRST_FUSE", fuse)
+    monkeypatch.setattr(E, "_FIRST_FUSE", "1" if fuse else "0")
     params = dict(m.named_parameters())
     with E.record_launches() as launches:
         out, saved = E.encoder_forward(m.plan, x, params, train=train)
@@ -60,7 +61,7 @@ def test_first_fuse_trainer_step_is_bitwise(cuda, monkeypatch):
     eps = torch.from_numpy(seeded_eps(3, 256)).to(cuda)
     out = {}
     for fuse in (True, False):
-        monkeypatch.setattr(E, "_FIRST_FUSE", fuse)
+        monkeypatch.setattr(E, "_FIRST_FUSE", "1" if fuse else "0")
         m.load_state_dict(sd)
         tr = VAETrainer(m, kl_lambda=5e-6)
         loss = tr.forward_backward(x, eps)
@@ -78,7 +79,7 @@ def test_first_fuse_encode_latents(cuda, monkeypatch):
     x = torch.from_numpy(synthetic_patterns(5, 64)).to(cuda)
     mu = {}
     for fuse in (True, False):
-        monkeypatch.setattr(E, "_FIRST_FUSE", fuse)
+        monkeypatch.setattr(E, "_FIRST_FUSE", "eval" if fuse else "0")
         with torch.no_grad():
             mu[fuse] = E.encode_latents(m.plan, x, params).cpu()
     assert torch.equal(mu[True], mu[False])

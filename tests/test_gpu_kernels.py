@@ -934,13 +934,17 @@ def test_fused_bwd_finalize_bitwise(cuda, B, H, cin, cout, pmode):
         assert torch.equal(a, b_)
 
 
-def test_network_end_matches_oracle(cuda):
+@pytest.mark.parametrize("H", [128, 256])
+@pytest.mark.parametrize("mfma", [True, False], ids=["mfma", "valu"])
+def test_network_end_matches_oracle(cuda, monkeypatch, H, mfma):
     """ebsdvae_net_end (the training step's network end in one pass over y13): x_hat of the final
     conv, the mean-BCE logit gradient g1, the per-band BCE sums, the last block's
     InstanceNorm-backward reduce (finalized here) and the final conv's gradient slices, against
-    the float64 oracle; then the apply pass it feeds gives the block's output gradient."""
+    the float64 oracle; then the apply pass it feeds gives the block's output gradient.  Both
+    forms: the split-fp16 MFMA kernel (default, round 6) and the fp32 VALU kernel (round 5)."""
+    monkeypatch.setattr(E, "_NET_END_MFMA", mfma)
     rng = np.random.default_rng(33)
-    B, H, C = 3, 128, 32
+    B, C = 3, 32
     y = rng.standard_normal((B, H, H, C)) * 1.3 - 0.4
     xh, mean, rstd = O.instance_norm(y)
     st = np.stack([mean[:, 0, 0, :], rstd[:, 0, 0, :]], -1)

@@ -29,6 +29,9 @@ CASES = {
     "fwd32to64p": ("fwd", 64, 32, 64, ACT_NORM_POOL),
     "fwd64to32u": ("fwd", 128, 64, 32, ACT_NORM_UP),
     "fwd32pool": ("fwdpool", 128, 32, 32, ACT_NORM),
+    # encoder.1 with its source recomputed from x (ebsdvae_conv3x3_fwd_split_first): the first
+    # conv's statistics only, no y0 read
+    "fwd32poolx": ("fwdfirst", 128, 32, 32, ACT_NORM),
     "fwd64pool": ("fwdpool", 64, 64, 64, ACT_NORM),
     "fwd128pool": ("fwdpool", 32, 128, 128, ACT_NORM),
     "fwd32to64n": ("fwd", 64, 32, 64, ACT_NORM),
@@ -67,9 +70,12 @@ def run(name, reps, pieces, B, warm=1.0):
     flops = 2.0 * B * H * H * cin * cout * 9
     w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) * 0.05
     bias = torch.zeros(cout, device=dev)
-    if kind in ("fwd", "fwdpool"):
+    if kind in ("fwd", "fwdpool", "fwdfirst"):
         Hs = 2 * H if mode == ACT_NORM_POOL else (H // 2 if mode == ACT_NORM_UP else H)
-        src = torch.randn(B, Hs, Hs, cin, device=dev, generator=g)
+        src = torch.randn(B, Hs, Hs, cin if kind != "fwdfirst" else 1, device=dev, generator=g)
+        w0 = torch.randn(cin, 1, 3, 3, device=dev, generator=g) * 0.3
+        b0 = torch.zeros(cin, device=dev)
+        st_out = torch.empty(B, cout, 2, device=dev)
         st = torch.stack([torch.zeros(B, cin, device=dev), torch.ones(B, cin, device=dev)], -1).contiguous()
         wp = torch.empty(N.call("ebsdvae_pack_split_bytes", cin, cout, pieces) // 4, device=dev)
         d = (N.PackDesc * 1)(N.PackDesc(w.data_ptr(), wp.data_ptr(), cin, cout, 0, 0))
@@ -81,6 +87,11 @@ def run(name, reps, pieces, B, warm=1.0):
         yp = torch.empty(B, H // 2, H // 2, cout, device=dev)
 
         def launch():
+            if kind == "fwdfirst":
+                N.call("ebsdvae_conv3x3_fwd_split_first", src.data_ptr(), st.data_ptr(), w0.data_ptr(),
+                       b0.data_ptr(), wp.data_ptr(), bias.data_ptr(), y.data_ptr(), yp.data_ptr(),
+                       part.data_ptr(), st_out.data_ptr(), B, H, H, cin, cout, pieces, s)
+                return
             if kind == "fwdpool":
                 N.call("ebsdvae_conv3x3_fwd_split_pooled", src.data_ptr(), st.data_ptr(), mode,
                        wp.data_ptr(), bias.data_ptr(), y.data_ptr(), yp.data_ptr(), part.data_ptr(),

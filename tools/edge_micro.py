@@ -66,6 +66,11 @@ def main():
                                    N.ptr(one), 1.0, N.ptr(ne_out[0]), N.ptr(ne_out[1]), N.ptr(ne_bce),
                                    ne_part.data_ptr(), N.ptr(ne_w), N.ptr(ne_b), B, H, H, C, s),
                     E4 + 3 * E4 // 32),
+        "net_end_valu": (lambda: N.call("ebsdvae_net_end_valu", N.ptr(y), N.ptr(st), N.ptr(w14), N.ptr(b),
+                                        N.ptr(x), N.ptr(one), 1.0, N.ptr(ne_out[0]), N.ptr(ne_out[1]),
+                                        N.ptr(ne_bce), ne_part.data_ptr(), N.ptr(ne_w), N.ptr(ne_b), B, H, H,
+                                        C, s),
+                         E4 + 3 * E4 // 32),
         # name: (launch, algorithmic bytes)
         "small1": (lambda: N.call("ebsdvae_conv3x3_fwd", N.ptr(x), None, ACT_RAW, N.ptr(w1), N.ptr(b),
                                   N.ptr(yc), N.ptr(spart), None, B, H, H, 1, C, s), E4 + E4 // 32),
