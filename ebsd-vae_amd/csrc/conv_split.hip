@@ -897,6 +897,7 @@ __global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_p
       float nb[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) nb[t] = xw[(t / 3) * (W + 2) + t % 3];
+#ifdef EV_FIRST_PK   // A/B: the channel pairs on v_pk_fma_f32 (first_conv_px2)
       pkf2 wa[9], wb[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
@@ -907,6 +908,19 @@ __global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_p
       const pkf2 yb = first_conv_px2(nb, wb, pk2(wq[9].z, wq[9].w));
       v = make_float4(normact_fs(ya.x, fs[0]), normact_fs(ya.y, fs[1]), normact_fs(yb.x, fs[2]),
                       normact_fs(yb.y, fs[3]));
+#else
+      // scalar v_fma_f32 chains (a packed fma beside MFMAs costs more issue than two scalar
+      // ones, MI355X_MICROARCH.md); each lane of first_conv_px2 is exactly this chain
+      float wc[4][9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        wc[0][t] = wq[t].x; wc[1][t] = wq[t].y; wc[2][t] = wq[t].z; wc[3][t] = wq[t].w;
+      }
+      v = make_float4(normact_fs(first_conv_px(nb, wc[0], wq[9].x), fs[0]),
+                      normact_fs(first_conv_px(nb, wc[1], wq[9].y), fs[1]),
+                      normact_fs(first_conv_px(nb, wc[2], wq[9].z), fs[2]),
+                      normact_fs(first_conv_px(nb, wc[3], wq[9].w), fs[3]));
+#endif
     } else {
       v = stage_value(slot_c, k, fs);
     }

@@ -389,10 +389,11 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
 // partials sum to the image's.  g1 is scaled by 2^kg (|g1| <= |cr| = the loss gradient scale,
 // known at launch) and the weights by 2^kw (their block-wide maximum) into fp16's range; both
 // are undone exactly.
-template <int W> constexpr int nm_urs() { return W + 8; }            // plane row: col c at c + 4
+template <int W> constexpr int nm_urs() { return W + 12; }  // plane row: col c at c + 4 (bank spread)
+template <int W> constexpr int nm_grs() { return W + 4; }   // g1 copy row (fp16, bank spread)
 template <int W> constexpr size_t nm_lds() {
   return (size_t)NE_RING * 9 * nm_urs<W>() * 4        // tap planes
-         + (size_t)NE_RING * 3 * 2 * W * 2              // g1 rows: [slot][kw][piece][W] fp16
+         + (size_t)NE_RING * 6 * nm_grs<W>() * 2        // g1 rows: [slot][kw][piece][GRS] fp16
          + (size_t)(W / 32) * 3 * 32 * 96;              // per-wave a0 / a1 / indicator images
 }
 constexpr int NM_IMG = 32 * 96;   // one per-wave image: 32 pixel rows of 32 channels (64 B + 32 pad)
@@ -414,6 +415,16 @@ EV_DEVINL f32x4 nm_mfma(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// Schedule: one barrier per source row.  Step i (source row q = r0 - 2 + i):
+//   [ (1) of row q: a, its fp16 pieces (registers), tap planes of row q -> plane slot q & 3 ]
+//   barrier
+//   [ x_hat / g1 of row q - 1 (planes of rows q - 2 .. q) -> g1 slot (q - 1) & 3;
+//     (2) of own row q - 3 (g1 rows q - 4 .. q - 2, written before the barrier of step i - 1 or
+//     earlier; its a fragments from the wave's image, written a step ago), then the image <- row
+//     q - 2 ]
+// Hazards: (1) of step i + 1 writes plane slot (q + 1) & 3 = (q - 3) & 3, which no wave reads
+// after the barrier of step i; the g1 slot written at step i + 1, q & 3 = (q - 4) & 3, was last
+// read by (2) of step i, before step i + 1's barrier.
 template <int W>
 __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
     const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
@@ -421,13 +432,13 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
     float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
   constexpr int C = NE_C, TH = NE_TH, NWAVE = W / 32, NTH = 64 * NWAVE;
-  constexpr int URS = nm_urs<W>(), UROWS = 9 * URS;
+  constexpr int URS = nm_urs<W>(), UROWS = 9 * URS, GRS = nm_grs<W>();
   extern __shared__ __attribute__((aligned(16))) float ne_sm[];
   float* uring = ne_sm;                                                   // [4][9][URS]
-  _Float16* gring = reinterpret_cast<_Float16*>(ne_sm + NE_RING * UROWS);  // [4][3][2][W]
+  _Float16* gring = reinterpret_cast<_Float16*>(ne_sm + NE_RING * UROWS);  // [4][3][2][GRS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, gq = lane >> 4;
-  char* img = reinterpret_cast<char*>(gring + NE_RING * 6 * W) + wave * 3 * NM_IMG;
+  char* img = reinterpret_cast<char*>(gring + NE_RING * 6 * GRS) + wave * 3 * NM_IMG;
   const int tile = blockIdx.x, b = blockIdx.y, T = gridDim.x;
   const int r0 = tile * TH;
   const size_t HW = (size_t)H * W;
@@ -468,14 +479,15 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
   const int kg = f16_shift_of(fabsf(cr));               // |g1| <= |cr|
   const float gsc = ldexpf(1.f, kg);
 
-  // zero columns of the tap planes (col -1 and W) and the two never-written g1 copy entries
+  // zero columns of the tap planes (col -1 and W), the two never-written g1 copy entries, and
+  // the image (row r0 - 3 has no own-row (2); a defined image keeps the first pass finite)
   for (int i = tid; i < NE_RING * 9 * 2; i += NTH) {
     const int rw = i >> 1;
     uring[rw * URS + ((i & 1) ? W + 4 : 3)] = 0.f;
   }
   if (tid < NE_RING * 2 * 2) {   // [slot][piece][copy 0 at W-1 | copy 2 at 0]
     const int sl = tid >> 2, pc = (tid >> 1) & 1, which = tid & 1;
-    gring[((sl * 3 + (which ? 2 : 0)) * 2 + pc) * W + (which ? 0 : W - 1)] = (_Float16)0.f;
+    gring[((sl * 3 + (which ? 2 : 0)) * 2 + pc) * GRS + (which ? 0 : W - 1)] = (_Float16)0.f;
   }
 
   const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + (size_t)b * HW * C), 0,
@@ -492,6 +504,13 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
   auto load_tgt = [&](int r, float& d) EV_LAMBDA_INLINE {
     d = (r >= 0 && r < H && xlane) ? xt[(size_t)b * HW + (size_t)r * W + px_w + lane] : 0.f;
   };
+  auto put_image = [&](const f16x8 (&pr)[3][2]) EV_LAMBDA_INLINE {
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+        *reinterpret_cast<f16x8*>(img + t3 * NM_IMG + (g * 16 + l16) * 96 + 16 * gq) = pr[t3][g];
+  };
 
   f32x4 G[2], P[2];
 #pragma unroll
@@ -500,27 +519,31 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
 #pragma unroll
   for (int t = 0; t < 9; ++t) S[t] = 0.f;
   float bsum = 0.f, bce = 0.f;
-  // a0 / a1 / indicator fragments of source rows q - 1 and q - 2 (rows of (2) two steps later)
-  f16x8 pa[3][2], pb[3][2];   // [tensor][group]; pa = row q - 1, pb = row q - 2
+  // a0 / a1 / indicator fragments of source rows q - 1 (pa) and q - 2 (pb)
+  f16x8 pa[3][2], pb[3][2], pn[3][2];
 #pragma unroll
   for (int t3 = 0; t3 < 3; ++t3)
 #pragma unroll
     for (int g = 0; g < 2; ++g) pa[t3][g] = pb[t3][g] = f16x8{};
+  put_image(pa);
   float4 ybuf[2][2][2];
   float tbuf[2];
   load_row(r0 - 2, ybuf[0]);
   load_row(r0 - 1, ybuf[1]);
+  // the target of row q - 1 is read at step i: tbuf[i & 1] holds row r0 - 3 + i
   load_tgt(r0 - 3, tbuf[0]);
   load_tgt(r0 - 2, tbuf[1]);
   // (2)'s g1 fragment geometry: tap t = l16 (t >= 9: zero), 4 + 4 pixels of the wave's 32
   const int tkh = l16 < 9 ? l16 / 3 : 0, tkw = l16 < 9 ? l16 % 3 : 0;
   const bool tlive = l16 < 9;
+  const int p4 = l16 & 3, qr = l16 >> 2;
+  const int px0 = 4 * gq + qr, px1 = px0 + 16;
   __syncthreads();
 
-  auto step = [&](int i, float4 (&ycur)[2][2], float& tcur, f16x8 (&pn)[3][2]) EV_LAMBDA_INLINE {
+  auto step = [&](int i, float4 (&ycur)[2][2], float& tcur) EV_LAMBDA_INLINE {
     const int q = r0 - 2 + i;
-    // ---- (1) a of source row q: registers (pn), tap planes into ring slot i & 3
-    if (q >= 0 && q < H) {   // block-uniform
+    // ---- (1) a of source row q: registers (pn), tap planes into ring slot q & 3
+    if (i < TH + 4 && q >= 0 && q < H) {   // block-uniform
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         float a[8];
@@ -557,12 +580,12 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
       u = nm_mfma(pn[0][g], wb1, u);
       u = nm_mfma(pn[0][g], wb0, u);
       if (tlive)   // C/D: rows (pixels) 4 gq .. 4 gq + 3 of the group, column l16 = tap
-        *reinterpret_cast<float4*>(uring + (i & 3) * UROWS + l16 * URS + 4 + px_w + g * 16 + 4 * gq) =
+        *reinterpret_cast<float4*>(uring + (q & 3) * UROWS + l16 * URS + 4 + px_w + g * 16 + 4 * gq) =
             make_float4(u[0] * uscale, u[1] * uscale, u[2] * uscale, u[3] * uscale);
     }
     __syncthreads();
-    // ---- x_hat, g1 and BCE of row q - 1 from the planes of rows q - 2 .. q
-    if (i >= 2) {
+    // ---- x_hat, g1 and BCE of row r = q - 1 from the planes of rows q - 2 .. q
+    if (i >= 2 && i < TH + 4) {
       const int r = q - 1;
       const bool inrow = r >= 0 && r < H, own = r >= r0 && r < r0 + TH;
       if (xlane) {
@@ -570,7 +593,7 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
         float xh = 0.f;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
-          const float* u = uring + ((i - 2 + kh) & 3) * UROWS + 4 + w - 1;
+          const float* u = uring + ((q - 2 + kh) & 3) * UROWS + 4 + w - 1;
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw) xh += u[(kh * 3 + kw) * URS + kw];
         }
@@ -586,7 +609,7 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
             bsum += g;
           }
         }
-        // S[t] = sum over own rows q of g1[q - d_t]: row r feeds tap row kh when
+        // S[t] = sum over own rows c of g1[c - d_t]: row r feeds tap row kh when
         // r in [r0 + 1 - kh, r0 + TH + 1 - kh), column w feeds kw unless the shifted
         // column falls outside the image (w = 0 for kw = 0, w = W - 1 for kw = 2)
 #pragma unroll
@@ -596,51 +619,39 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
             if (w != 0) S[3 * kh] += g;
             if (w != W - 1) S[3 * kh + 2] += g;
           }
-        // g1 * 2^kg as two fp16 pieces into the three column-shifted copies of ring slot r & 3:
+        // g1 * 2^kg as two fp16 pieces into the three column-shifted copies of slot r & 3:
         // copy kw holds g1[x + 1 - kw] at x
         const float gs = g * gsc;
         const _Float16 q0 = (_Float16)gs;
         const _Float16 q1 = (_Float16)(gs - (float)q0);
-        _Float16* gr = gring + (size_t)(r & 3) * 6 * W;
+        _Float16* gr = gring + (size_t)(r & 3) * 6 * GRS;
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const int x = w - 1 + kw;
           if (x >= 0 && x < W) {
-            gr[(kw * 2 + 0) * W + x] = q0;
-            gr[(kw * 2 + 1) * W + x] = q1;
+            gr[(kw * 2 + 0) * GRS + x] = q0;
+            gr[(kw * 2 + 1) * GRS + x] = q1;
           }
         }
       }
     }
-    load_tgt(q + 1, tcur);   // x_hat row q + 1 is computed at step i + 2
-    __syncthreads();
-    // ---- (2) G and P of own row q - 2 (its fragments in pb)
-    if (i >= 4) {
-      const int qo = q - 2;
-      // the row's a0 / a1 / indicator as pixel-major images (this wave's 32 pixels)
-#pragma unroll
-      for (int t3 = 0; t3 < 3; ++t3)
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-          *reinterpret_cast<f16x8*>(img + t3 * NM_IMG + (g * 16 + l16) * 96 + 16 * gq) = pb[t3][g];
-      __builtin_amdgcn_sched_barrier(0);
-      // g1 fragment: tap t = l16 at pixels 4 gq + j and 16 + 4 gq + j (the transposed reads'
-      // K order), row qo - kh + 1
-      const _Float16* gr = gring + (size_t)((qo - tkh + 1) & 3) * 6 * W + px_w + 4 * gq;
+    load_tgt(q + 1, tcur);   // row q + 1 is x_hat'd at step i + 2 (slot (i + 2) & 1)
+    // ---- (2) G and P of own row c = q - 3 (its fragments in the wave's image)
+    if (i >= 5 && i < TH + 5) {   // c in [r0, r0 + TH)
+      const int c = q - 3;
+      const _Float16* gr = gring + (size_t)((c - tkh + 1) & 3) * 6 * GRS + px_w + 4 * gq;
       typedef short s16x4 __attribute__((ext_vector_type(4)));
       typedef short s16x8 __attribute__((ext_vector_type(8)));
       f16x8 gb[2];
 #pragma unroll
       for (int pc = 0; pc < 2; ++pc) {
-        const _Float16* gp = gr + (tkw * 2 + pc) * W;
+        const _Float16* gp = gr + (tkw * 2 + pc) * GRS;
         const s16x4 lo = *reinterpret_cast<const s16x4*>(gp);
         const s16x4 hi = *reinterpret_cast<const s16x4*>(gp + 16);
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         if (!tlive) v = s16x8{};
         gb[pc] = __builtin_bit_cast(f16x8, v);
       }
-      const int p4 = l16 & 3, qr = l16 >> 2;
-      const int px0 = 4 * gq + qr, px1 = px0 + 16;
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb) {
         const int col = (16 * mb + 4 * p4) * 2;
@@ -653,18 +664,20 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
         P[mb] = nm_mfma(ai, gb[1], P[mb]);
         P[mb] = nm_mfma(ai, gb[0], P[mb]);
       }
-      (void)qo;
     }
+    // the image now takes row q - 2, (2)'s row at step i + 1 (this wave's own LDS region: its
+    // reads above were issued first and a wave's LDS operations complete in order)
+    __builtin_amdgcn_sched_barrier(0);
+    put_image(pb);
 #pragma unroll
     for (int t3 = 0; t3 < 3; ++t3)
 #pragma unroll
       for (int g = 0; g < 2; ++g) { pb[t3][g] = pa[t3][g]; pa[t3][g] = pn[t3][g]; }
   };
-  f16x8 pn[3][2];
 #pragma unroll 1
-  for (int i = 0; i < TH + 4; i += 2) {
-    step(i, ybuf[0], tbuf[0], pn);
-    step(i + 1, ybuf[1], tbuf[1], pn);
+  for (int i = 0; i < TH + 6; i += 2) {
+    step(i, ybuf[0], tbuf[0]);
+    step(i + 1, ybuf[1], tbuf[1]);
   }
   __syncthreads();
   // ---- band partials, fixed order
