@@ -325,6 +325,90 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(
   }
 }
 
+
+// ------------------------------------------------------------------ first-conv statistics (inference)
+// The InstanceNorm statistics of y0 = conv(x, w0) + b0 without y0 (ebsdvae_conv_first_stats):
+// every channel is a linear map of the 9 shifted copies of x, so with, per image,
+//   m_t  = (1/N) sum_p xs_t[p]          and   Q_tt' = (1/N) sum_p xs_t[p] xs_t'[p]
+// (xs_t[p] = x[p + d_t], zero outside the image; 9 sums and 45 products per pixel, for all 32
+// channels at once instead of 288 MACs per pixel, in double: FP64 FMAs run at half the fp32 rate)
+//   mean_c = b_c + sum_t w_ct m_t,   var_c = sum_{t,t'} w_ct w_ct' (Q_tt' - m_t m_t')
+// in double (no cancellation to speak of).  Every thread accumulates its column's pixels in
+// double; the block's 256 threads fold in a fixed order.  The inference path's first conv then reads x once and writes 256 bytes per image
+// (encoder.1 recomputes y0 from x, ebsdvae_conv3x3_fwd_split_first).
+constexpr int FG_CH = 32;            // rows per chunk (LDS tile FG_CH + 2 rows)
+constexpr int FG_NS = 9 + 45;        // sums per image
+__global__ __launch_bounds__(256) void first_gram_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ w0,
+                                                         const float* __restrict__ b0,
+                                                         float2* __restrict__ st, int C, int H, int W) {
+  extern __shared__ float fg_sm[];   // x tile [FG_CH + 2][W + 2], then the fold scratch
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int WP = W + 2;
+  const float* xb = x + (size_t)b * H * W;
+  const int rpc = 256 / W;            // rows of a chunk a column's threads split (W <= 256)
+  const int col = tid % W, r_off = tid / W;
+  double acc[FG_NS];
+#pragma unroll
+  for (int e = 0; e < FG_NS; ++e) acc[e] = 0.0;
+  for (int h0 = 0; h0 < H; h0 += FG_CH) {
+    __syncthreads();
+    for (int i = tid; i < (FG_CH + 2) * WP; i += 256) {
+      const int r = i / WP, cc = i - r * WP;
+      const int gh = h0 - 1 + r, gw = cc - 1;
+      fg_sm[i] = (gh >= 0 && gh < H && gw >= 0 && gw < W) ? xb[gh * W + gw] : 0.f;
+    }
+    __syncthreads();
+    if (r_off < rpc) {
+      for (int r = r_off; r < FG_CH; r += rpc) {
+        double nb[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) nb[t] = (double)fg_sm[(r + t / 3) * WP + col + t % 3];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] += nb[t];
+#pragma unroll
+        for (int t = 0, e = 9; t < 9; ++t)
+#pragma unroll
+          for (int u = t; u < 9; ++u, ++e) acc[e] = fma(nb[t], nb[u], acc[e]);
+      }
+    }
+  }
+  __syncthreads();
+  // fixed-order fold: lanes by a shuffle tree, then the 4 waves
+  double* red = reinterpret_cast<double*>(fg_sm);   // [4][FG_NS]
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int e = 0; e < FG_NS; ++e) {
+    double v = acc[e];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wave * FG_NS + e] = v;
+  }
+  __syncthreads();
+  double* tot = red + 4 * FG_NS;                     // [FG_NS]
+  if (tid < FG_NS) tot[tid] = ((red[tid] + red[FG_NS + tid]) + red[2 * FG_NS + tid]) + red[3 * FG_NS + tid];
+  __syncthreads();
+  if (tid < C) {
+    const int c = tid;
+    const double inv_n = 1.0 / ((double)H * W);
+    double m[9], w[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) { m[t] = tot[t] * inv_n; w[t] = (double)w0[c * 9 + t]; }
+    double mean = b0 ? (double)b0[c] : 0.0, var = 0.0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) mean += w[t] * m[t];
+    int e = 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int u = t; u < 9; ++u, ++e) {
+        const double cov = tot[e] * inv_n - m[t] * m[u];
+        var += (t == u ? 1.0 : 2.0) * w[t] * w[u] * cov;
+      }
+    var = var > 0.0 ? var : 0.0;
+    st[(size_t)b * C + c] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)kInEps)));
+  }
+}
 }  // namespace ev
 
 using namespace ev;
@@ -383,4 +467,16 @@ extern "C" int ebsdvae_conv3x3_cout1_dgrad(const float* g1, const float* w, floa
   hipLaunchKernelGGL(conv_cout1_dgrad_kernel<32>, dim3(tiles), dim3(256), lds, (hipStream_t)stream,
                      g1, w, gin, B, H, W, g);
   return evh::check_launch("conv3x3_cout1_dgrad");
+}
+
+extern "C" int ebsdvae_conv_first_stats(const float* x, const float* w0, const float* b0, float* st,
+                                        int B, int H, int W, int C, ebsdvae_stream_t stream) {
+  EV_REQUIRE(x && w0 && st && B > 0 && C == FIRST_C, "conv_first_stats: bad args (C must be %d)", FIRST_C);
+  EV_REQUIRE(W >= 8 && W <= 256 && 256 % W == 0 && H % FG_CH == 0 && ev_dim_ok(H),
+             "conv_first_stats: %dx%d unsupported (W must divide 256, H a multiple of %d)", H, W, FG_CH);
+  const size_t lds = (size_t)(FG_CH + 2) * (W + 2) * sizeof(float);
+  const size_t lds_fold = (size_t)5 * FG_NS * sizeof(double);
+  hipLaunchKernelGGL(first_gram_kernel, dim3(B), dim3(256), lds > lds_fold ? lds : lds_fold,
+                     (hipStream_t)stream, x, w0, b0, (float2*)st, C, H, W);
+  return evh::check_launch("conv_first_stats");
 }

@@ -32,6 +32,7 @@ SIGNATURES = {
     "ebsdvae_stream_destroy_cus": [P],
     "ebsdvae_conv_first_stat_tiles": [I, I],
     "ebsdvae_conv_first_fwd": [P, P, P, P, P, I, I, I, I, P],
+    "ebsdvae_conv_first_stats": [P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_apply_wgrad_rc": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_happly_wgrad_rc": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "ebsdvae_in_bwd_first_happly_wgrad": [P, P, P, P, P, P, P, I, I, I, I, P],

@@ -466,10 +466,23 @@ def _first_valu(layer: ConvLayer) -> bool:
             and N.call("ebsdvae_conv_first_stat_tiles", layer.H, layer.H) > 0)
 
 
+# statistics-only first conv (inference): from x's shifted moments in double
+# (ebsdvae_conv_first_stats) instead of the fma-chain kernel with its y0 store skipped;
+# EBSDVAE_FIRST_GRAM=0 keeps the latter (A/B; bit-identical statistics to training's)
+_FIRST_GRAM = os.environ.get("EBSDVAE_FIRST_GRAM", "1") != "0"
+
+
 def _conv_first(x, layer: ConvLayer, w, b, B, write_y=True):
     """write_y=False: the InstanceNorm statistics only (y None) -- the next conv recomputes y
     from x (conv_forward_first)."""
     H = layer.H
+    if not write_y and _FIRST_GRAM and H % 32 == 0 and 256 % H == 0:
+        st = _empty(B, layer.cout, 2, like=w)
+        _launch("conv3x3_fwd", conv_flops(B, H, H, 1, layer.cout), N.call, "ebsdvae_conv_first_stats",
+                N.ptr(x), N.ptr(w), N.ptr(b), N.ptr(st), B, H, H, layer.cout, N.stream(),
+                tag=f"fwd  {layer.name:13s} {layer.cin:3d}->{layer.cout:3d} @{H:3d} m0 stats",
+                nbytes=4 * x.numel())
+        return None, st
     T = N.call("ebsdvae_conv_first_stat_tiles", H, H)
     y = _empty(B, H, H, layer.cout, like=w) if write_y else None
     part = _empty(B, T, layer.cout, 2, like=w)

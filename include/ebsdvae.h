@@ -124,6 +124,14 @@ int ebsdvae_conv3x3_dgrad_inbwd(const float* g, const float* wpack, float* gin,
  * ebsdvae_in_bwd_first_apply_wgrad_rc and ebsdvae_conv3x3_fwd_split_first recompute y with.
  * y may be NULL: the statistics only (inference, where the next conv recomputes y from x). */
 int ebsdvae_conv_first_stat_tiles(int H, int W);
+/* The InstanceNorm statistics st (B, C) {mean, rstd} of y0 = the first conv of x (C == 32)
+ * without computing y0: from the 9 shifted means and the 45 shifted second moments of x per
+ * image, in double (mean_c = b_c + sum_t w_ct m_t, var_c = sum_tt' w_ct w_ct' cov_tt').  The
+ * inference path's first conv (y0 is recomputed by ebsdvae_conv3x3_fwd_split_first).  Needs W
+ * dividing 256 and H % 32 == 0. */
+int ebsdvae_conv_first_stats(const float* x, const float* w0, const float* b0, float* st, int B,
+                             int H, int W, int C, ebsdvae_stream_t stream);
+
 int ebsdvae_conv_first_fwd(const float* x, const float* w0, const float* b0, float* y,
                            float* part, int B, int H, int W, int C, ebsdvae_stream_t stream);
 int ebsdvae_conv3x3_cout1_fwd(const float* src, const float* src_stats, int src_mode,

@@ -147,7 +147,9 @@ def test_encoder_only_latents_vs_reference(cuda, name, prec):
     mu = m.encode_mu(torch.from_numpy(f["x"]).to(cuda))
     assert O.rel_err(h(mu), f["mu"]) < 1e-4
     _, _, mu_full, _ = m(torch.from_numpy(f["x"]).to(cuda), eps=torch.from_numpy(f["eps"]).to(cuda))
-    assert torch.allclose(mu, mu_full.detach(), rtol=0, atol=1e-6)
+    # the inference path takes the first block's statistics from x's moments in double
+    # (ebsdvae_conv_first_stats), the training forward from its fp32 two-pass sums: rounding apart
+    assert O.rel_err(h(mu), h(mu_full)) < 2e-5
 
 
 @pytest.mark.parametrize("scale", [1.0, 1e-3])
