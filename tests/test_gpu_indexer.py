@@ -43,15 +43,20 @@ def test_inference_forward_defers_the_decoder(cuda):
         assert x_hat.shape == (6, 1, 128, 128) and x_hat.dtype == torch.float32 and x_hat.is_cuda
         n_enc = len(launched)
         assert n_enc == len(m.plan.enc)       # the encoder's convs, nothing of the decoder
+        # the inference path takes the first block's statistics from x's moments in double
+        # (ebsdvae_conv_first_stats), the training-mode forward from its fp32 two-pass sums:
+        # the two agree to rounding, not bit for bit
+        def rel(a, b):
+            return float((a - b).abs().max() / b.abs().max())
         for a, b in ((mu, mu_t), (std, std_t), (z, z_t)):
-            assert torch.allclose(a, b, rtol=0, atol=1e-6)
+            assert rel(a, b) < 2e-5
         with E.record_launches() as launched:
             xh = x_hat.detach().cpu()
         assert len(launched) > 0 and x_hat.materialized
-        assert torch.allclose(xh, xh_t.cpu(), rtol=0, atol=1e-5)
+        assert rel(xh, xh_t.cpu()) < 5e-5
         # the deferred value behaves as a tensor in the reference's consumers
-        assert torch.allclose(torch.sigmoid(x_hat), torch.sigmoid(xh_t), atol=1e-5)
-        assert np.allclose(x_hat.cpu().numpy(), xh_t.cpu().numpy(), atol=1e-5)
+        assert torch.allclose(torch.sigmoid(x_hat), torch.sigmoid(xh_t), atol=5e-5)
+        assert np.allclose(x_hat.cpu().numpy(), xh_t.cpu().numpy(), rtol=5e-5, atol=5e-5)
     # encode_mu is the same computation
     assert torch.allclose(m.encode_mu(x), mu, rtol=0, atol=1e-6)
 

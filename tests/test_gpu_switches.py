@@ -100,7 +100,11 @@ def test_arithmetic_switch_meets_pinned_gates(cuda, monkeypatch, switch, prec):
 
 def test_inference_switches_keep_outputs(cuda, monkeypatch):
     """EBSDVAE_EVAL_Y=1 (pooled producers also write y in inference) and
-    EBSDVAE_DEFER_DECODE=0 (x_hat computed at model(x)): bitwise the default outputs."""
+    EBSDVAE_DEFER_DECODE=0 (x_hat computed at model(x)): bitwise the default outputs.  The
+    first block's statistics from its fma chain (EBSDVAE_FIRST_GRAM=0) in both: with the
+    deferral off the call takes the training-mode encoder, whose statistics are the fp32
+    two-pass ones, not the inference path's moment-based ones."""
+    monkeypatch.setattr(E, "_FIRST_GRAM", False)
     f, m = _model(cuda)
     m.eval()
     x = torch.from_numpy(f["x"]).to(cuda)
