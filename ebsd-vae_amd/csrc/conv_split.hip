@@ -404,6 +404,10 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
   // input-gradient launches (a fused IN-backward reduce or the summed upsample adjoint) pass no
   // statistics partials (spart == nullptr)
   constexpr bool FUSED = FP == P_ID || FP == P_POOL || FP == P_UP || FP == FP_UPSUM;
+#ifndef EV_EPI_OPAQUE
+#define EV_EPI_OPAQUE 1
+#endif
+  constexpr bool EPI_OPAQUE = EV_EPI_OPAQUE && FP == FP_POOLOUT;
   if constexpr (PH == 1) {   // loads only: the offsets of the PH 0 / 2 code below
     const int nf = 0;
     const int co = co_base + l32;
@@ -471,6 +475,12 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
     // fused input gradients write h (below); pooled inference writes ypool only (one uniform
     // branch, not one per value)
     if (!FUSED && (FP != FP_POOLOUT || y)) {
+      // pooled producers: the per-lane store offsets are tile-invariant, and hipcc hoists every
+      // one of them out of the tile loop (16 + 8 per fragment column) -- the registers the
+      // 64-channel producer then spilled.  An opaque copy of the base keeps them in the epilogue
+      // (base + constant, mostly folded into the store's immediate offset)
+      int vb = vbase;
+      if constexpr (EPI_OPAQUE) asm volatile("" : "+v"(vb));
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
@@ -479,7 +489,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
           // element 0 -- hipcc / ROCm 7.2)
           const float v = acc[mf][nf][r];
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry,
-                                                vbase + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, kEpiPol);
+                                                vb + (mf * mfs + (r & 3) + 8 * (r >> 2)) * NT * 4, 0, kEpiPol);
         }
     }
     if (FP == FP_UPSUM) {
@@ -539,13 +549,15 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
       for (int m0 = 0; m0 < MF; m0 += 2) {
         if (W >= 32) {   // fragment m0 = tile row 2rp, fragment m0 + 1 = row 2rp + 1, same 32 columns
           const int prow = (wpx0 / W + m0) >> 1, pcol = (wpx0 % W + 4 * hk) >> 1;
+          int pb = ((prow * W2 + pcol) * NT + co) * 4;
+          if constexpr (EPI_OPAQUE) asm volatile("" : "+v"(pb));
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const float m = fmaxf(fmaxf(acc[m0][nf][r], acc[m0][nf][r + 1]),
                                   fmaxf(acc[m0 + 1][nf][r], acc[m0 + 1][nf][r + 1]));
-            const int pc = pcol + (((r & 3) + 8 * (r >> 2)) >> 1);
+            const int dc = ((r & 3) + 8 * (r >> 2)) >> 1;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rq,
-                                                  ((prow * W2 + pc) * NT + co) * 4, 0, kEpiPol);
+                                                  pb + dc * NT * 4, 0, kEpiPol);
           }
         } else {         // W == 16: a fragment is two rows; the window is r, r+1, r+8, r+9
 #pragma unroll

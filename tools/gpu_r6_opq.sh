@@ -1,0 +1,14 @@
+# round 6: opaque epilogue store offsets of the pooled producers (no spill) -- parity, micro, bench A/B
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_gpu_kernels.py tests/test_gpu_trainer.py tests/test_gpu_first_fuse.py > gpurun_out/r6_opq_tests.txt 2>&1 || { echo TESTS_FAILED; tail -20 gpurun_out/r6_opq_tests.txt; exit 1; }
+tail -1 gpurun_out/r6_opq_tests.txt
+for i in 1 2; do for L in default noopq; do
+  if [ $L = default ]; then unset EBSDVAE_LIB; else export EBSDVAE_LIB=ebsd-vae_amd/lib/libebsdvae_$L.so; fi
+  timeout -k 10 150 python3 tools/conv_micro.py --pieces 16 --warm 0.5 --only fwd32pool,fwd64pool,fwd128pool,fwd32poolx 2>&1 | grep -v amdgpu.ids | sed "s/^/$L /" || exit 1
+  timeout -k 10 200 python3 bench.py --no-cpu-baseline --strict-fp32-steps 0 --c4-batches 256 --c5-steps 0 --steps 20 > gpurun_out/opq_$L.txt 2>/dev/null || exit 1
+  echo "$L bench $(python3 -c "import json;d=json.loads(open('gpurun_out/opq_$L.txt').read().splitlines()[-1]);print(d['ms_per_step'], d['c4_encoder_latents']['ms_per_batch'])")"
+done; done
