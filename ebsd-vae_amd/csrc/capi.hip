@@ -38,17 +38,18 @@ extern "C" const char* ebsdvae_last_error(void) { return g_err; }
 extern "C" int ebsdvae_version(void) { return EBSDVAE_ABI_VERSION; }
 
 // ------------------------------------------------------------------ cross-stream ordering
-// `waiter` waits for the work enqueued on `signaler` so far, through an event recorded with a
-// device-scope release (hipEventReleaseToDevice) instead of the default system-scope fence:
-// both streams run on this device, so nothing needs to become visible to the host, and the
-// system-scope writeback + invalidate of every fork / join costs the GPU a few microseconds of
-// idle time (tools/step_gaps.py).  A wait takes the event's state at enqueue time, so a small
+// `waiter` waits for the work enqueued on `signaler` so far, through an event recorded with the
+// default system-scope release (round 6; EBSDVAE_FORK_DEVICE_SCOPE=1 selects the device-scope
+// release, hipEventReleaseToDevice, used through round 5: the same step time either way, and the
+// system scope takes the one non-default synchronisation choice off the side-stream path whose
+// single unexplained stale read DESIGN.md section 13 records).  A wait takes the event's state at
+// enqueue time, so a small
 // ring of events per device is reused round-robin; capturable into hipGraphs (fork / join).
 // The ring is the signaler stream's device's (not the caller's current device), created
 // on that device; ring creation and the round-robin index are guarded, since forward and
 // autograd-backward threads both fork and join.
 namespace {
-// ring[kind][device]: kind 0 = fork / join events (device-scope release, no timing), kind 1 =
+// ring[kind][device]: kind 0 = fork / join events (no timing), kind 1 =
 // kernel-attached fork events (signalled by the completion of the launch they are attached to)
 constexpr int kRing = 64, kMaxDev = 64;
 hipEvent_t g_ring[2][kMaxDev][kRing];
@@ -74,10 +75,10 @@ int ring_event(ebsdvae_stream_t signaler, int kind, hipEvent_t* out) {
       return 2;
     }
     bool ok = true;
+    const char* ds = getenv("EBSDVAE_FORK_DEVICE_SCOPE");
+    const unsigned f0 = hipEventDisableTiming | ((ds && ds[0] == '1') ? hipEventReleaseToDevice : 0u);
     for (int i = 0; i < kRing && ok; ++i)
-      ok = hipEventCreateWithFlags(&g_ring[kind][dev][i],
-                                   kind == 0 ? (hipEventDisableTiming | hipEventReleaseToDevice)
-                                             : hipEventDefault) == hipSuccess;
+      ok = hipEventCreateWithFlags(&g_ring[kind][dev][i], kind == 0 ? f0 : hipEventDefault) == hipSuccess;
     (void)hipSetDevice(cur);
     if (!ok) {
       evh::set_error("stream_wait: hipEventCreateWithFlags failed");

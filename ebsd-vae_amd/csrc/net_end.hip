@@ -27,7 +27,13 @@ namespace ev {
 
 // rows per band: the two recomputed halo rows above and below cost 4 / TH of the band's work
 constexpr int NE_C = 32, NE_TH = 32;
-constexpr int NE_RING = 4;                 // ring slots (a and g1): slot(row) = (row - r0 + k) & 3
+constexpr int NE_RING = 4;
+#ifndef EV_NE_UNROLL6
+#define EV_NE_UNROLL6 1
+#endif
+#ifndef EV_NE_BRFREE
+#define EV_NE_BRFREE 1
+#endif                 // ring slots (a and g1): slot(row) = (row - r0 + k) & 3
 // per width: threads, ring row (zero column, W pixels, zero column)
 template <int W> constexpr int ne_nth() { return 2 * W; }
 template <int W> constexpr int ne_wp() { return W + 2; }
@@ -390,7 +396,7 @@ __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
 // known at launch) and the weights by 2^kw (their block-wide maximum) into fp16's range; both
 // are undone exactly.
 template <int W> constexpr int nm_urs() { return W + 12; }  // plane row: col c at c + 4 (bank spread)
-template <int W> constexpr int nm_grs() { return W + 4; }   // g1 copy row (fp16, bank spread)
+template <int W> constexpr int nm_grs() { return W + 8; }   // g1 copy row (fp16): x at x + 4
 template <int W> constexpr size_t nm_lds() {
   return (size_t)NE_RING * 9 * nm_urs<W>() * 4        // tap planes
          + (size_t)NE_RING * 6 * nm_grs<W>() * 2        // g1 rows: [slot][kw][piece][GRS] fp16
@@ -485,9 +491,9 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
     const int rw = i >> 1;
     uring[rw * URS + ((i & 1) ? W + 4 : 3)] = 0.f;
   }
-  if (tid < NE_RING * 2 * 2) {   // [slot][piece][copy 0 at W-1 | copy 2 at 0]
+  if (tid < NE_RING * 2 * 2) {   // [slot][piece][copy 0 at x = W-1 | copy 2 at x = 0] (x at x + 4)
     const int sl = tid >> 2, pc = (tid >> 1) & 1, which = tid & 1;
-    gring[((sl * 3 + (which ? 2 : 0)) * 2 + pc) * GRS + (which ? 0 : W - 1)] = (_Float16)0.f;
+    gring[((sl * 3 + (which ? 2 : 0)) * 2 + pc) * GRS + (which ? 4 : W + 3)] = (_Float16)0.f;
   }
 
   const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + (size_t)b * HW * C), 0,
@@ -520,12 +526,14 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
   for (int t = 0; t < 9; ++t) S[t] = 0.f;
   float bsum = 0.f, bce = 0.f;
   // a0 / a1 / indicator fragments of source rows q - 1 (pa) and q - 2 (pb)
-  f16x8 pa[3][2], pb[3][2], pn[3][2];
+  // three register sets in rotation (step i: row q in R[i % 3], q - 1 in R[(i - 1) % 3], q - 2
+  // in R[(i - 2) % 3]); the loop is unrolled by 6 so the rotation is a renaming, not copies
+  f16x8 R0[3][2], R1[3][2], R2[3][2];
 #pragma unroll
   for (int t3 = 0; t3 < 3; ++t3)
 #pragma unroll
-    for (int g = 0; g < 2; ++g) pa[t3][g] = pb[t3][g] = f16x8{};
-  put_image(pa);
+    for (int g = 0; g < 2; ++g) R0[t3][g] = R1[t3][g] = R2[t3][g] = f16x8{};
+  put_image(R2);
   float4 ybuf[2][2][2];
   float tbuf[2];
   load_row(r0 - 2, ybuf[0]);
@@ -538,9 +546,12 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
   const bool tlive = l16 < 9;
   const int p4 = l16 & 3, qr = l16 >> 2;
   const int px0 = 4 * gq + qr, px1 = px0 + 16;
+  // S[t]: column w feeds tap column kw = 0 unless w == 0, kw = 2 unless w == W - 1
+  const float ml = (px_w + lane) != 0 ? 1.f : 0.f, mr = (px_w + lane) != W - 1 ? 1.f : 0.f;
   __syncthreads();
 
-  auto step = [&](int i, float4 (&ycur)[2][2], float& tcur) EV_LAMBDA_INLINE {
+  auto step = [&](int i, float4 (&ycur)[2][2], float& tcur, f16x8 (&pn)[3][2], const f16x8 (&pb)[3][2])
+                  EV_LAMBDA_INLINE {
     const int q = r0 - 2 + i;
     // ---- (1) a of source row q: registers (pn), tap planes into ring slot q & 3
     if (i < TH + 4 && q >= 0 && q < H) {   // block-uniform
@@ -612,6 +623,16 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
         // S[t] = sum over own rows c of g1[c - d_t]: row r feeds tap row kh when
         // r in [r0 + 1 - kh, r0 + TH + 1 - kh), column w feeds kw unless the shifted
         // column falls outside the image (w = 0 for kw = 0, w = W - 1 for kw = 2)
+#if EV_NE_BRFREE
+        const float gl = g * ml, gr_ = g * mr;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+          if (r >= r0 + 1 - kh && r < r0 + TH + 1 - kh) {   // block-uniform
+            S[3 * kh + 1] += g;
+            S[3 * kh] += gl;
+            S[3 * kh + 2] += gr_;
+          }
+#else
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh)
           if (r >= r0 + 1 - kh && r < r0 + TH + 1 - kh) {
@@ -619,18 +640,23 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
             if (w != 0) S[3 * kh] += g;
             if (w != W - 1) S[3 * kh + 2] += g;
           }
+#endif
         // g1 * 2^kg as two fp16 pieces into the three column-shifted copies of slot r & 3:
-        // copy kw holds g1[x + 1 - kw] at x
+        // copy kw holds g1[x + 1 - kw] at x, stored at x + 4 (8-byte aligned fragment reads): the
+        // writes to x = -1 and x = W land in pad entries no fragment reads, so they need no test
         const float gs = g * gsc;
         const _Float16 q0 = (_Float16)gs;
         const _Float16 q1 = (_Float16)(gs - (float)q0);
-        _Float16* gr = gring + (size_t)(r & 3) * 6 * GRS;
+        _Float16* gr = gring + (size_t)(r & 3) * 6 * GRS + w + 3;
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
+#if !EV_NE_BRFREE
           const int x = w - 1 + kw;
-          if (x >= 0 && x < W) {
-            gr[(kw * 2 + 0) * GRS + x] = q0;
-            gr[(kw * 2 + 1) * GRS + x] = q1;
+          if (x >= 0 && x < W)
+#endif
+          {
+            gr[(kw * 2 + 0) * GRS + kw] = q0;
+            gr[(kw * 2 + 1) * GRS + kw] = q1;
           }
         }
       }
@@ -639,7 +665,7 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
     // ---- (2) G and P of own row c = q - 3 (its fragments in the wave's image)
     if (i >= 5 && i < TH + 5) {   // c in [r0, r0 + TH)
       const int c = q - 3;
-      const _Float16* gr = gring + (size_t)((c - tkh + 1) & 3) * 6 * GRS + px_w + 4 * gq;
+      const _Float16* gr = gring + (size_t)((c - tkh + 1) & 3) * 6 * GRS + px_w + 4 * gq + 4;
       typedef short s16x4 __attribute__((ext_vector_type(4)));
       typedef short s16x8 __attribute__((ext_vector_type(8)));
       f16x8 gb[2];
@@ -648,8 +674,8 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
         const _Float16* gp = gr + (tkw * 2 + pc) * GRS;
         const s16x4 lo = *reinterpret_cast<const s16x4*>(gp);
         const s16x4 hi = *reinterpret_cast<const s16x4*>(gp + 16);
-        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (!tlive) v = s16x8{};
+        // (tap columns t >= 9 of G / P are never read: their lanes' clamped reads need no zeroing)
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         gb[pc] = __builtin_bit_cast(f16x8, v);
       }
 #pragma unroll
@@ -669,16 +695,36 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
     // reads above were issued first and a wave's LDS operations complete in order)
     __builtin_amdgcn_sched_barrier(0);
     put_image(pb);
+  };
+  static_assert((TH + 6) % 6 == 2, "six-step loop plus two");
+#if !EV_NE_UNROLL6
+  auto rot = [&]() EV_LAMBDA_INLINE {
 #pragma unroll
     for (int t3 = 0; t3 < 3; ++t3)
 #pragma unroll
-      for (int g = 0; g < 2; ++g) { pb[t3][g] = pa[t3][g]; pa[t3][g] = pn[t3][g]; }
+      for (int g = 0; g < 2; ++g) { R2[t3][g] = R1[t3][g]; R1[t3][g] = R0[t3][g]; }
   };
+  (void)R2;
 #pragma unroll 1
   for (int i = 0; i < TH + 6; i += 2) {
-    step(i, ybuf[0], tbuf[0]);
-    step(i + 1, ybuf[1], tbuf[1]);
+    step(i, ybuf[0], tbuf[0], R0, R2);
+    rot();
+    step(i + 1, ybuf[1], tbuf[1], R0, R2);
+    rot();
   }
+#else
+#pragma unroll 1
+  for (int i = 0; i < TH + 4; i += 6) {
+    step(i, ybuf[0], tbuf[0], R0, R1);
+    step(i + 1, ybuf[1], tbuf[1], R1, R2);
+    step(i + 2, ybuf[0], tbuf[0], R2, R0);
+    step(i + 3, ybuf[1], tbuf[1], R0, R1);
+    step(i + 4, ybuf[0], tbuf[0], R1, R2);
+    step(i + 5, ybuf[1], tbuf[1], R2, R0);
+  }
+  step(TH + 4, ybuf[0], tbuf[0], R0, R1);
+  step(TH + 5, ybuf[1], tbuf[1], R1, R2);
+#endif
   __syncthreads();
   // ---- band partials, fixed order
   // G / P: C/D of wave w, M block mb: channel 16 mb + 4 gq + k (k = 0..3), tap l16

@@ -43,8 +43,8 @@ const char* ebsdvae_last_error(void);
 int ebsdvae_version(void);
 
 /* ---- stream ordering ------------------------------------------------------------------
- * `waiter` waits for the work enqueued on `signaler` so far (an event with a device-scope
- * release: cheaper than the default system-scope fence of torch's Stream.wait_stream).
+ * `waiter` waits for the work enqueued on `signaler` so far (an event with the default
+ * system-scope release; EBSDVAE_FORK_DEVICE_SCOPE=1: device scope, as through round 5).
  * Used for the weight-gradient side stream's fork / join (latice/engine.py); capturable. */
 int ebsdvae_stream_wait(ebsdvae_stream_t waiter, ebsdvae_stream_t signaler);
 /* Kernel-attached fork (no record packet on the signaler): arm, launch the InstanceNorm-backward
