@@ -26,7 +26,17 @@
 namespace ev {
 
 // rows per band: the two recomputed halo rows above and below cost 4 / TH of the band's work
-constexpr int NE_C = 32, NE_TH = 32;
+// band rows: 64 where H allows (round 6: the recomputed halo rows are 6 of every 70 steps
+// instead of 6 of 38), else 32
+#ifndef EV_NE_TH
+#define EV_NE_TH 64
+#endif
+constexpr int NE_C = 32, NE_TH = EV_NE_TH, NE_TH_MIN = 32;
+#ifndef EV_NE_FOLD
+#define EV_NE_FOLD 16
+#endif
+constexpr int NE_FOLD = EV_NE_FOLD;   // rows per running sum of net_end_mfma_kernel (power of two)
+constexpr int ne_th(int H) { return H % NE_TH == 0 ? NE_TH : NE_TH_MIN; }
 constexpr int NE_RING = 4;
 #ifndef EV_NE_UNROLL6
 #define EV_NE_UNROLL6 1
@@ -94,13 +104,13 @@ EV_DEVINL float ne_x1(float v) { return ne_dpp<0xB1>(v); }
 // activation-ring kernel moved 784 B of LDS per thread and row, this one 180.  Measured (PMC,
 // B = 256): 207 vs 216 us -- both are VALU-issue-bound (668 VALU per wave and row, 216 of them
 // the three 288-MAC-per-pixel contractions), not LDS-bound.
-template <int W>
+template <int W, int TH>
 __global__ __launch_bounds__(ne_nth<W>(), W == 128 ? 2 : 1) void net_end_kernel(
     const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
     const float* __restrict__ b14, const float* __restrict__ xt, const float* __restrict__ g_loss,
     float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
-  constexpr int C = NE_C, TH = NE_TH, WP = ne_wp<W>(), UROW = ne_urow<W>();
+  constexpr int C = NE_C, WP = ne_wp<W>(), UROW = ne_urow<W>();
   constexpr int NE_NTH = ne_nth<W>(), NPL = W / 4, NWAVE = NE_NTH / 64;
   extern __shared__ __attribute__((aligned(16))) float ne_sm[];
   float* uring = ne_sm;                       // [4][9][WP]
@@ -431,13 +441,13 @@ EV_DEVINL f32x4 nm_mfma(f16x8 a, f16x8 b, f32x4 c) {
 // Hazards: (1) of step i + 1 writes plane slot (q + 1) & 3 = (q - 3) & 3, which no wave reads
 // after the barrier of step i; the g1 slot written at step i + 1, q & 3 = (q - 4) & 3, was last
 // read by (2) of step i, before step i + 1's barrier.
-template <int W>
+template <int W, int TH>
 __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
     const float* __restrict__ y, const float2* __restrict__ st, const float* __restrict__ w14,
     const float* __restrict__ b14, const float* __restrict__ xt, const float* __restrict__ g_loss,
     float gscale, float* __restrict__ x_hat, float* __restrict__ g1out, float* __restrict__ bce_part,
     double2* __restrict__ part, float* __restrict__ wpart, float* __restrict__ bpart, int H) {
-  constexpr int C = NE_C, TH = NE_TH, NWAVE = W / 32, NTH = 64 * NWAVE;
+  constexpr int C = NE_C, NWAVE = W / 32, NTH = 64 * NWAVE;
   constexpr int URS = nm_urs<W>(), UROWS = 9 * URS, GRS = nm_grs<W>();
   extern __shared__ __attribute__((aligned(16))) float ne_sm[];
   float* uring = ne_sm;                                                   // [4][9][URS]
@@ -518,12 +528,16 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
         *reinterpret_cast<f16x8*>(img + t3 * NM_IMG + (g * 16 + l16) * 96 + 16 * gq) = pr[t3][g];
   };
 
-  f32x4 G[2], P[2];
+  // G / P / S over the band's rows: the running sums of NE_FOLD rows at a time (G, P, S) are
+  // folded into a second set (G2, P2, S2), so no fp32 sum runs over more rows than the 32-row
+  // bands' did (64 rows in one accumulator took the saturated fixture's zero-bias residue of
+  // decoder.13 from inside its gate to 22.8 x 2^-24 A)
+  f32x4 G[2], P[2], G2[2], P2[2];
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb) G[mb] = P[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float S[9];
+  for (int mb = 0; mb < 2; ++mb) G[mb] = P[mb] = G2[mb] = P2[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float S[9], S2[9];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) S[t] = 0.f;
+  for (int t = 0; t < 9; ++t) S[t] = S2[t] = 0.f;
   float bsum = 0.f, bce = 0.f;
   // a0 / a1 / indicator fragments of source rows q - 1 (pa) and q - 2 (pb)
   // three register sets in rotation (step i: row q in R[i % 3], q - 1 in R[(i - 1) % 3], q - 2
@@ -690,13 +704,25 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
         P[mb] = nm_mfma(ai, gb[1], P[mb]);
         P[mb] = nm_mfma(ai, gb[0], P[mb]);
       }
+      if constexpr (TH > NE_FOLD) {
+        if (((i - 5) & (NE_FOLD - 1)) == NE_FOLD - 1) {   // block-uniform
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) {
+            G2[mb] += G[mb];
+            P2[mb] += P[mb];
+            G[mb] = P[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int t = 0; t < 9; ++t) { S2[t] += S[t]; S[t] = 0.f; }
+        }
+      }
     }
     // the image now takes row q - 2, (2)'s row at step i + 1 (this wave's own LDS region: its
     // reads above were issued first and a wave's LDS operations complete in order)
     __builtin_amdgcn_sched_barrier(0);
     put_image(pb);
   };
-  static_assert((TH + 6) % 6 == 2, "six-step loop plus two");
+  constexpr int NS = TH + 6, NM = NS - NS % 6;   // steps; those of the six-step loop
 #if !EV_NE_UNROLL6
   auto rot = [&]() EV_LAMBDA_INLINE {
 #pragma unroll
@@ -705,8 +731,9 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
       for (int g = 0; g < 2; ++g) { R2[t3][g] = R1[t3][g]; R1[t3][g] = R0[t3][g]; }
   };
   (void)R2;
+  static_assert(NS % 2 == 0, "two-step loop");
 #pragma unroll 1
-  for (int i = 0; i < TH + 6; i += 2) {
+  for (int i = 0; i < NS; i += 2) {
     step(i, ybuf[0], tbuf[0], R0, R2);
     rot();
     step(i + 1, ybuf[1], tbuf[1], R0, R2);
@@ -714,7 +741,7 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
   }
 #else
 #pragma unroll 1
-  for (int i = 0; i < TH + 4; i += 6) {
+  for (int i = 0; i < NM; i += 6) {
     step(i, ybuf[0], tbuf[0], R0, R1);
     step(i + 1, ybuf[1], tbuf[1], R1, R2);
     step(i + 2, ybuf[0], tbuf[0], R2, R0);
@@ -722,8 +749,11 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
     step(i + 4, ybuf[0], tbuf[0], R1, R2);
     step(i + 5, ybuf[1], tbuf[1], R2, R0);
   }
-  step(TH + 4, ybuf[0], tbuf[0], R0, R1);
-  step(TH + 5, ybuf[1], tbuf[1], R1, R2);
+  if constexpr (NS % 6 > 0) step(NM, ybuf[0], tbuf[0], R0, R1);
+  if constexpr (NS % 6 > 1) step(NM + 1, ybuf[1], tbuf[1], R1, R2);
+  if constexpr (NS % 6 > 2) step(NM + 2, ybuf[0], tbuf[0], R2, R0);
+  if constexpr (NS % 6 > 3) step(NM + 3, ybuf[1], tbuf[1], R0, R1);
+  if constexpr (NS % 6 > 4) step(NM + 4, ybuf[0], tbuf[0], R1, R2);
 #endif
   __syncthreads();
   // ---- band partials, fixed order
@@ -735,8 +765,8 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int c = 16 * mb + 4 * gq + k;
-        red[((wave * 2 + 0) * 32 + c) * 16 + l16] = G[mb][k];
-        red[((wave * 2 + 1) * 32 + c) * 16 + l16] = P[mb][k];
+        red[((wave * 2 + 0) * 32 + c) * 16 + l16] = G2[mb][k] + G[mb][k];
+        red[((wave * 2 + 1) * 32 + c) * 16 + l16] = P2[mb][k] + P[mb][k];
       }
   }
   // S, bsum, bce: the 32 pixel lanes by a shuffle tree, then the waves
@@ -744,7 +774,7 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
   {
     float v[11];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) v[t] = S[t];
+    for (int t = 0; t < 9; ++t) v[t] = S2[t] + S[t];
     v[9] = bsum;
     v[10] = bce;
 #pragma unroll
@@ -799,15 +829,15 @@ __global__ __launch_bounds__(2 * W, W == 128 ? 2 : 1) void net_end_mfma_kernel(
 using namespace ev;
 
 extern "C" int ebsdvae_net_end_tiles(int H, int W) {
-  return ((W == 128 || W == 256) && ev_dim_ok(H) && H % NE_TH == 0) ? H / NE_TH : -1;
+  return ((W == 128 || W == 256) && ev_dim_ok(H) && H % NE_TH_MIN == 0) ? H / ne_th(H) : -1;
 }
 
-template <int W, bool MF>
+template <int W, int TH, bool MF>
 static void net_end_launch(dim3 grid, hipStream_t st, const float* y13, const float* st13,
                            const float* w14, const float* b14, const float* x, const float* g_loss,
                            float gscale, float* x_hat, float* g1, float* bce_part, double* part,
                            float* wpart, float* bpart, int H) {
-  auto k = MF ? net_end_mfma_kernel<W> : net_end_kernel<W>;
+  auto k = MF ? net_end_mfma_kernel<W, TH> : net_end_kernel<W, TH>;
   constexpr size_t lds = MF ? nm_lds<W>() : ne_lds_u<W>();
   static bool once = false;
   if (!once) {
@@ -827,15 +857,19 @@ static int net_end_entry(const float* y13, const float* st13, const float* w14, 
   EV_REQUIRE(y13 && st13 && w14 && x && x_hat && g1 && bce_part && part && wpart && bpart && B > 0,
              "net_end: null pointer");
   EV_REQUIRE(C == NE_C && ebsdvae_net_end_tiles(H, W) > 0,
-             "net_end: C=%d %dx%d unsupported (C 32, W 128 or 256, H a multiple of %d)", C, H, W, NE_TH);
+             "net_end: C=%d %dx%d unsupported (C 32, W 128 or 256, H a multiple of %d)", C, H, W, NE_TH_MIN);
   const int T = ebsdvae_net_end_tiles(H, W);
   const float gscale = scale / ((float)B * (float)(H * W));
-  if (W == 128)
-    net_end_launch<128, MF>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale,
-                            x_hat, g1, bce_part, part, wpart, bpart, H);
-  else
-    net_end_launch<256, MF>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale,
-                            x_hat, g1, bce_part, part, wpart, bpart, H);
+  const bool big = ne_th(H) == NE_TH;
+#define EV_NE_LAUNCH(WW, TT)                                                                            \
+  net_end_launch<WW, TT, MF>(dim3(T, B), (hipStream_t)stream, y13, st13, w14, b14, x, g_loss, gscale, \
+                             x_hat, g1, bce_part, part, wpart, bpart, H)
+  if (W == 128) {
+    if (big) EV_NE_LAUNCH(128, NE_TH); else EV_NE_LAUNCH(128, NE_TH_MIN);
+  } else {
+    if (big) EV_NE_LAUNCH(256, NE_TH); else EV_NE_LAUNCH(256, NE_TH_MIN);
+  }
+#undef EV_NE_LAUNCH
   return evh::check_launch("net_end");
 }
 

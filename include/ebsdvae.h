@@ -465,7 +465,8 @@ int ebsdvae_vae_loss_fwd_parts(const float* bce_part, int tiles, const float* z,
 
 /* ---- network end of the training step (latice/model.py:147-148 + lightning_module.py:79-92) --
  * One pass over the last block's pre-norm output y13 (B, H, W, C) NHWC with its statistics
- * st13 {mean, rstd} (B, C), for C == 32, W == 128 or 256, H % 32 == 0:
+ * st13 {mean, rstd} (B, C), for C == 32, W == 128 or 256, H % 32 == 0 (row bands of 64 rows
+ * where H % 64 == 0, else 32; T = ebsdvae_net_end_tiles(H, W)):
  *   x_hat (B, 1, H, W) = Conv2d(32, 1)(lrelu(IN(y13))) with w14 (1, 32, 3, 3), b14 (1) or NULL;
  *   g1 (B, H, W) = g_loss * scale / (B * H * W) * (sigmoid(x_hat) - x), the gradient of the
  *     mean-BCE part of the loss w.r.t. the logits (g_loss a device scalar, NULL = 1);
