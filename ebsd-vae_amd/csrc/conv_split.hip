@@ -637,6 +637,19 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
   }
 }
 
+// WREG (round 6): the one-image 8x8 configuration (4 waves of 64 px x 32 co, one block per CU)
+// loads its weight fragments straight into registers (each lane's 16-byte B fragment of every
+// k-step, 40 VGPRs per chunk, double-buffered by chunk parity) instead of DMA-ing the 40-KiB
+// slab into LDS and reading it back: the four waves need disjoint 32-channel column blocks of
+// it, so the LDS round trip carried no reuse, and its writes and reads were half of the
+// iteration's LDS traffic (EV_WREG=0: the LDS slab, A/B)
+#ifndef EV_WREG
+#define EV_WREG 1
+#endif
+constexpr bool pipe_wreg(int NWV, int WM, int NF, int NI, int WR) {
+  return EV_WREG && NWV == 4 && WM == 1 && NF == 1 && NI == 1 && WR == 0;
+}
+
 // Persistent, software-pipelined form of conv3x3_split_kernel (same tiles, LDS layouts,
 // MFMA sequence and epilogue, so its results are bit-identical).  Each block owns a
 // contiguous run of tiles (row bands; consecutive ones are neighbouring bands of one image,
@@ -656,7 +669,7 @@ EV_DEVINL void pipe_epilogue(f32x16 (&acc)[MF][NF], const float* __restrict__ bi
 //   and stay resident (Cin = 32 layers, where they fit beside the halo buffers): no weight
 //   DMA per iteration (its issue cost sits in every iteration's instruction stream)
 template <int NP, int NWV, int WM, int MF, int NF, int KX, int MODE, int FP, int NI, int WR>
-__global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_pipe_kernel(
+__global__ __launch_bounds__(NWV * 64, (MODE == ACT_FIRST || pipe_wreg(NWV, WM, NF, NI, WR)) ? 1 : 2) void conv3x3_pipe_kernel(
     const float* __restrict__ src, const float2* __restrict__ sstats, const char* __restrict__ wp,
     const float* __restrict__ bias, float* __restrict__ y, float2* __restrict__ spart,
     float* __restrict__ act_out, int B, int H, int W, int Cin, int TH, int tpb,
@@ -988,8 +1001,23 @@ __global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_p
   const auto rwp = __builtin_amdgcn_make_buffer_rsrc((void*)wp, 0, nch * WSLAB, 0x00020000);
   // NP_F16: the layer's weight shift k (weights packed as w * 2^k), in the pack's trailer
   const int wshift = NP == NP_F16 ? *reinterpret_cast<const int*>(wp + (size_t)nch * WSLAB) : 0;
+  constexpr bool WREG = pipe_wreg(NWV, WM, NF, NI, WR);
+  bf16x8 wreg[WREG ? 2 : 1][WREG ? 5 : 1][NPC];
+  auto issue_wreg = [&](int it, auto slot_c) EV_LAMBDA_INLINE {
+    constexpr int sl = decltype(slot_c)::value;
+    const int ch = it & (nch - 1);
+    const int nc = wn * NF * 32 + l32;   // this lane's output channel (B fragment column)
+#pragma unroll
+    for (int s5 = 0; s5 < 5; ++s5) {
+      const int t = 2 * s5 + hk;
+#pragma unroll
+      for (int i = 0; i < NPC; ++i)
+        wreg[sl][s5][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rwp, ch * WSLAB + ((t * NPC + i) * NT + nc) * 16, 0, 0));
+    }
+  };
   auto issue_weights = [&](int it, char* lw) EV_LAMBDA_INLINE {
-    if constexpr (WR) return;   // resident since the prologue
+    if constexpr (WR || WREG) return;   // resident since the prologue / in registers
     const int ch = it & (nch - 1);
 #pragma unroll
     for (int j = 0; j < WPER; ++j) {
@@ -1064,6 +1092,7 @@ __global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_p
       if ((it & (nch - 1)) == nch - 1) epi_prefetch(it);
 #ifndef EV_PIPE_LATE_ISSUE
     issue_weights(it1, lw0 + (1 - P) * WSLABP);
+    if constexpr (WREG) issue_wreg(it1, std::integral_constant<int, WREG ? 1 - P : 0>());
     issue_halo(itp, std::integral_constant<int, SL_LD>());
 #endif
     EV_TACC(tr_issue, tb0);
@@ -1086,12 +1115,17 @@ __global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_p
 #pragma unroll
         for (int i = 0; i < NPC; ++i) a[i][mf] = lds_frag(pa + 16 * i);
       }
-      const int t = 2 * s + hk;
+      if constexpr (WREG) {
 #pragma unroll
-      for (int nf = 0; nf < NF; ++nf) {
-        const char* pb = lw + ((t * NPC) * NT + ncol + nf * 32) * 16;
+        for (int i = 0; i < NPC; ++i) b[i][0] = wreg[WREG ? P : 0][WREG ? s : 0][i];
+      } else {
+        const int t = 2 * s + hk;
 #pragma unroll
-        for (int i = 0; i < NPC; ++i) b[i][nf] = lds_frag(pb + i * NT * 16);
+        for (int nf = 0; nf < NF; ++nf) {
+          const char* pb = lw + ((t * NPC) * NT + ncol + nf * 32) * 16;
+#pragma unroll
+          for (int i = 0; i < NPC; ++i) b[i][nf] = lds_frag(pb + i * NT * 16);
+        }
       }
     };
     if constexpr (FPF) load_frags(0, fa[0], fb[0]);
@@ -1239,6 +1273,8 @@ __global__ __launch_bounds__(NWV * 64, MODE == ACT_FIRST ? 1 : 2) void conv3x3_p
     for (int pc = wave_u; pc < WR * WSLAB / 1024; pc += NWV)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rwp, (lds_void_ptr)(lw0 + pc * 1024), 16,
                                                pc * 1024 + lane * 16, 0, 0, 0);
+  } else if constexpr (WREG) {
+    issue_wreg(0, std::integral_constant<int, 0>());
   } else {
     issue_weights(0, lw0);
   }
