@@ -37,15 +37,16 @@ DECISION_GATE = 1e-3
 STATE_GATE = 1e-4
 # residue gate, in units of 2^-24 * A_c, per conv arithmetic (the one in effect when check_grads
 # runs).  Measured on MI355X (round 4, every fixture, B = 4..256, every switch): f16x3 <= 3.0,
-# bf16x6 <= 1.7, fp32 <= 1.4.  One fp32 run (round 4, gpurun_out/t_sw1.txt) returned 180.8 on
-# decoder.13.0 with a 200x weight-gradient error on the same layer while the layers whose
-# gradients flow through decoder.13's gy were exact: decoder.13's side-stream weight gradient
-# read a gy13 different from the one the main stream's input gradient read -- a read that did
-# not see its producer's final values (DESIGN.md section 13 gives the analysis).  No run since
-# has repeated it; the poison-mode suite (tests/test_gpu_poison.py, and every repeat of
-# tests/test_gpu_determinism.py) turns such a read into NaN instead of an in-tolerance error.
-# The reference's own fp32 run at B = 256: 0.18 (bias_noise_b256.npz).  A 16x margin over the
-# worst measured value of every arithmetic.
+# bf16x6 <= 1.7, fp32 <= 1.4.  Round 6's MFMA network end forms the last block's reduce sums
+# from a two-piece fp16 g1: <= 1.1 on the well-conditioned fixtures, 5.3 / 6.7 / 9.0 (f16x3 /
+# bf16x6 / fp32) on the saturated vae128_b2_edge, on decoder.13.0.  One fp32 run (round 5,
+# gpurun_out/t_sw1.txt) returned 180.8 on decoder.13.0 with a 200x weight-gradient error on the
+# same layer while the layers whose gradients flow through decoder.13's gy were exact: most
+# likely decoder.13's side-stream weight gradient read a gy13 that differed from the one the
+# main stream's input gradient read; the cause is not established.  No
+# run since has repeated it; the poison-mode suite (tests/test_gpu_poison.py, and every repeat
+# of tests/test_gpu_determinism.py) turns such a read into NaN instead of an in-tolerance error.
+# The reference's own fp32 run at B = 256: 0.18 (bias_noise_b256.npz).
 ZERO_BIAS_K = {"f16x3": 16.0, "bf16x6": 16.0, "bf16x3": 16.0, "fp32": 16.0}
 U32 = 2.0 ** -24
 
