@@ -59,6 +59,9 @@ def main():
     cases = {
         "first_valu": (lambda: N.call("ebsdvae_conv_first_fwd", N.ptr(x), N.ptr(w0), N.ptr(b), N.ptr(yc),
                                       N.ptr(fpart), B, H, H, C, s), E4 + E4 // 32),
+        # inference's first-conv statistics from the moments of x (reads x only)
+        "first_stats": (lambda: N.call("ebsdvae_conv_first_stats", N.ptr(x), N.ptr(w0), N.ptr(b),
+                                       N.ptr(fpart), B, H, H, C, s), E4 // 32),
         "first_rc": (lambda: N.call("ebsdvae_in_bwd_first_apply_wgrad_rc", N.ptr(y2), N.ptr(w0), N.ptr(b),
                                     N.ptr(st), N.ptr(bst), N.ptr(x), N.ptr(wpart), N.ptr(bpart),
                                     B, H, H, C, s), E4 + E4 // 32),
