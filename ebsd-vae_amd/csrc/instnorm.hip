@@ -334,31 +334,37 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
     return (LG && p < p1) ? ld4_nt(gsrc + ((size_t)b * H * W + p) * C + c)
                           : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  float4 ycur[U], gcur[U];
+  // two register sets, swapped by a two-group loop (no copies between groups)
+  float4 yA[U], gA[U], yB[U], gB[U];
   if (PF) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      ycur[u] = ldy(p0 + pr + u * NPR);
-      gcur[u] = ldg(p0 + pr + u * NPR);
+      if constexpr (!RC) yA[u] = ldy(p0 + pr + u * NPR);
+      gA[u] = ldg(p0 + pr + u * NPR);
     }
   }
-  for (int pg = p0 + pr; pg < p1; pg += U * NPR) {
-    float4 ynxt[U], gnxt[U];
+  // the pixel's (row, column), advanced by NPR per pixel (W is a multiple of NPR = 32, so a
+  // step wraps at most once): no per-pixel division
+  int ph = (p0 + pr) / W, pw = (p0 + pr) - ph * W;
+  auto group = [&](int pg, float4 (&ycur)[U], float4 (&gcur)[U], float4 (&ynxt)[U],
+                   float4 (&gnxt)[U]) EV_LAMBDA_INLINE {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (PF) {
-        ynxt[u] = ldy(pg + (U + u) * NPR);
+        if constexpr (!RC) ynxt[u] = ldy(pg + (U + u) * NPR);
         gnxt[u] = ldg(pg + (U + u) * NPR);
       } else {
-        ycur[u] = ldy(pg + u * NPR);
+        if constexpr (!RC) ycur[u] = ldy(pg + u * NPR);
         gcur[u] = ldg(pg + u * NPR);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
     const int p = pg + u * NPR;
+    const int h = ph, w = pw;
+    pw += NPR;
+    if (pw >= W) { pw -= W; ++ph; }
     if (p >= p1) break;
-    const int h = p / W, w = p - h * W;
     float nb[9];   // FINAL: g1[q - d(tap)] ; FIRST: x[p + d(tap)]
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -383,9 +389,11 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       const float4 g4 = gcur[u];
       ga[0] = g4.x; ga[1] = g4.y; ga[2] = g4.z; ga[3] = g4.w;
     }
-    const float4 y4 = ycur[u];
-    float yy[4] = {y4.x, y4.y, y4.z, y4.w};
-    if (RC) {
+    float yy[4];
+    if constexpr (!RC) {
+      const float4 y4 = ycur[u];
+      yy[0] = y4.x; yy[1] = y4.y; yy[2] = y4.z; yy[3] = y4.w;
+    } else {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const pkf2 y2 = first_conv_px2(nb, wv2[k], bb2[k]);
@@ -421,10 +429,11 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
       amax = fmaxf(fmaxf(amax, fmaxf(fabsf(o[0]), fabsf(o[1]))), fmaxf(fabsf(o[2]), fabsf(o[3])));
     }
     }
-    if (PF) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) { ycur[u] = ynxt[u]; gcur[u] = gnxt[u]; }
-    }
+  };
+  for (int pg = p0 + pr; pg < p1; pg += 2 * U * NPR) {
+    group(pg, yA, gA, yB, gB);
+    if (pg + U * NPR >= p1) break;
+    group(pg + U * NPR, yB, gB, yA, gA);
   }
   const int slice = b * T + tile;
   if (FUSE_ == FUSE_FINAL && APPLY && gmax) {   // block-uniform: one maximum per (image, tile)
@@ -499,7 +508,8 @@ __global__ __launch_bounds__(256) void in_bwd_edge_kernel(
 
 // dynamic LDS of in_bwd_edge_kernel: the 1-channel source of one row band + halo
 static size_t edge_lds(int H, int W, int T) { return (size_t)(H / T + 2) * (W + 2) * sizeof(float); }
-static bool edge_ok(int H, int W, int T) { return (H / T + 2) * (W + 2) <= 256 * EDGE_NB_ITEMS; }
+// (W a multiple of the 32 pixel rows of a block: the kernel steps its pixel coordinates by 32)
+static bool edge_ok(int H, int W, int T) { return W % 32 == 0 && (H / T + 2) * (W + 2) <= 256 * EDGE_NB_ITEMS; }
 
 static int grid_for(size_t n4) {
   size_t g = (n4 + 255) / 256;
@@ -639,7 +649,7 @@ extern "C" int ebsdvae_in_bwd_final_reduce(const float* g1, const float* w14, co
   EV_REQUIRE(g1 && w14 && y && stats && part && wpart && bpart && C == 32,
              "in_bwd_final_reduce: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: %dx%d unsupported (W a multiple of 32, row band too large)", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, false>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)nullptr,
                      (const float*)nullptr, (double2*)part, wpart, bpart, (float*)nullptr, H, W, T,
@@ -653,7 +663,7 @@ extern "C" int ebsdvae_in_bwd_final_apply(const float* g1, const float* w14, con
   EV_REQUIRE(g1 && w14 && y && stats && bstats && gy && C == 32,
              "in_bwd_final_apply: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: %dx%d unsupported (W a multiple of 32, row band too large)", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)bstats,
                      (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
@@ -672,7 +682,7 @@ extern "C" int ebsdvae_in_bwd_final_apply_max(const float* g1, const float* w14,
   EV_REQUIRE(g1 && w14 && y && stats && bstats && gy && gmax && C == 32,
              "in_bwd_final_apply_max: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: %dx%d unsupported (W a multiple of 32, row band too large)", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FINAL, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, g1, w14, y, (const float2*)stats, (const float2*)bstats,
                      (const float*)nullptr, (double2*)nullptr, (float*)nullptr, (float*)nullptr, gy,
@@ -688,7 +698,7 @@ extern "C" int ebsdvae_in_bwd_first_apply_wgrad_rc(const float* gnext, const flo
   EV_REQUIRE(gnext && w0 && stats && bstats && x && wpart && bpart && C == 32,
              "in_bwd_first_apply_wgrad_rc: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: %dx%d unsupported (W a multiple of 32, row band too large)", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST_RC, true>), dim3(T, B), dim3(256),
                      edge_lds(H, W, T), (hipStream_t)stream, gnext, w0, (const float*)nullptr,
                      (const float2*)stats, (const float2*)bstats, x, (double2*)nullptr, wpart, bpart,
@@ -705,7 +715,7 @@ extern "C" int ebsdvae_in_bwd_first_happly_wgrad_rc(const float* h, const float*
   EV_REQUIRE(h && w0 && stats && bstats && x && wpart && bpart && C == 32,
              "in_bwd_first_happly_wgrad_rc: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: %dx%d unsupported (W a multiple of 32, row band too large)", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST_RC, true, true>), dim3(T, B), dim3(256),
                      edge_lds(H, W, T), (hipStream_t)stream, h, w0, (const float*)nullptr,
                      (const float2*)stats, (const float2*)bstats, x, (double2*)nullptr, wpart, bpart,
@@ -720,7 +730,7 @@ extern "C" int ebsdvae_in_bwd_first_happly_wgrad(const float* h, const float* y,
   EV_REQUIRE(h && y && stats && bstats && x && wpart && bpart && C == 32,
              "in_bwd_first_happly_wgrad: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: %dx%d unsupported (W a multiple of 32, row band too large)", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, h, (const float*)nullptr, y, (const float2*)stats,
                      (const float2*)bstats, x, (double2*)nullptr, wpart, bpart, (float*)nullptr, H, W,
@@ -735,7 +745,7 @@ extern "C" int ebsdvae_in_bwd_first_apply_wgrad(const float* gnext, const float*
   EV_REQUIRE(gnext && y && stats && bstats && x && wpart && bpart && C == 32,
              "in_bwd_first_apply_wgrad: bad args (C must be 32)");
   const int T = in_bwd_tiles_host(H, W);
-  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: row band of %dx%d too large", H, W);
+  EV_REQUIRE(edge_ok(H, W, T), "in_bwd edge: %dx%d unsupported (W a multiple of 32, row band too large)", H, W);
   hipLaunchKernelGGL((in_bwd_edge_kernel<FUSE_FIRST, true>), dim3(T, B), dim3(256), edge_lds(H, W, T),
                      (hipStream_t)stream, gnext, (const float*)nullptr, y, (const float2*)stats,
                      (const float2*)bstats, x, (double2*)nullptr, wpart, bpart, (float*)nullptr, H, W,
