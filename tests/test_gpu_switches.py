@@ -135,6 +135,7 @@ LIB_SWITCHES = [
     ("EBSDVAE_WG_CO128", "0", "f16x3", 1),
     ("EBSDVAE_WG_TW", "32", "bf16x6", 1),
     ("EBSDVAE_WG_BLOCKS", "1024", "f16x3", 64),
+    ("EBSDVAE_FORK_DEVICE_SCOPE", "1", "f16x3", 1),   # round 6: device-scope fork events (A/B)
 ]
 
 
