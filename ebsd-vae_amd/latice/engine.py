@@ -813,6 +813,9 @@ def deferred_side_join(device):
         _join_side(device)
 
 
+# EBSDVAE_FINAL_REDUCE_SIDE=1: the encoder's last reduction batch on the side stream as through
+# round 6's middle (A/B)
+_ON_MAIN_FINAL = os.environ.get("EBSDVAE_FINAL_REDUCE_SIDE", "0") in ("", "0")
 # Weight-gradient slice reductions queued inside `batched_wgrad_reduce()` run as ONE batched
 # pair of launches when the block exits (ebsdvae_wgrad_reduce_batch) instead of two launches
 # per layer; outside such a block they run immediately.  Results are bit-identical.
@@ -820,7 +823,10 @@ _RQ = None
 
 
 @contextlib.contextmanager
-def batched_wgrad_reduce():
+def batched_wgrad_reduce(on_main: bool = False):
+    """on_main: the batch is the step's last work (the encoder backward): it runs on the current
+    stream after one join of the side stream, instead of on the side stream behind a fork of the
+    current one and joined again (two cross-stream hops, ≈13 µs each at the end of the step)."""
     global _RQ
     outer, q = _RQ, []
     _RQ = q
@@ -828,13 +834,15 @@ def batched_wgrad_reduce():
         yield
     finally:
         _RQ = outer
-        _flush_reduces(q)
+        _flush_reduces(q, on_main=on_main)
 
 
-def _flush_reduces(q):
+def _flush_reduces(q, on_main: bool = False):
     if not q:
         return
     dev = q[0][0].device
+    if on_main and _ON_MAIN_FINAL and _side_pending(dev):
+        _join_side(dev)   # the weight gradients' partials are complete once the side stream is
     side = side_stream(dev) if _side_pending(dev) else None
     if side is not None:
         # behind the weight gradients on the side stream; partials made on the current
@@ -1263,7 +1271,7 @@ def encoder_backward(plan: Plan, g_enc, x, saved, params, grads=None, need_gx=Fa
     {layer name: callable}: once that layer's weight gradient is issued, the reductions queued
     so far are flushed (on the stream the weight gradients run on) and the callable runs -- the
     trainer starts the all-reduce of the gradients finished by then (trainer.py)."""
-    with batched_wgrad_reduce():
+    with batched_wgrad_reduce(on_main=True):
         return _encoder_backward(plan, g_enc, x, saved, params, grads, need_gx, packs,
                                  after_wgrad or {})
 

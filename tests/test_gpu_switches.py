@@ -50,10 +50,11 @@ def _grad(m, f, device, copies=1):
     return tr, rec
 
 
-@pytest.mark.parametrize("attr", ["_KFORK", "_LIGHT_EVENTS", "_WG_STREAM"])
+@pytest.mark.parametrize("attr", ["_KFORK", "_LIGHT_EVENTS", "_WG_STREAM", "_ON_MAIN_FINAL"])
 @pytest.mark.parametrize("copies", [1, 64], ids=["B4", "B256"])
 def test_schedule_switch_gives_bitwise_equal_gradients(cuda, monkeypatch, attr, copies):
-    """EBSDVAE_KFORK=0 / EBSDVAE_LIGHT_EVENTS=0 / EBSDVAE_WGRAD_STREAM=0 against the default."""
+    """EBSDVAE_KFORK=0 / EBSDVAE_LIGHT_EVENTS=0 / EBSDVAE_WGRAD_STREAM=0 /
+    EBSDVAE_FINAL_REDUCE_SIDE=1 against the default."""
     f, m = _model(cuda)
     tr0, _ = _grad(m, f, cuda, copies)
     g0 = tr0.gflat.clone()
