@@ -33,7 +33,7 @@ namespace ev {
 #endif
 constexpr int NE_C = 32, NE_TH = EV_NE_TH, NE_TH_MIN = 32;
 #ifndef EV_NE_FOLD
-#define EV_NE_FOLD 16
+#define EV_NE_FOLD 8
 #endif
 constexpr int NE_FOLD = EV_NE_FOLD;   // rows per running sum of net_end_mfma_kernel (power of two)
 constexpr int ne_th(int H) { return H % NE_TH == 0 ? NE_TH : NE_TH_MIN; }

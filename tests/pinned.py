@@ -38,7 +38,7 @@ STATE_GATE = 1e-4
 # residue gate, in units of 2^-24 * A_c, per conv arithmetic (the one in effect when check_grads
 # runs).  Measured on MI355X (round 4, every fixture, B = 4..256, every switch): f16x3 <= 3.0,
 # bf16x6 <= 1.7, fp32 <= 1.4.  Round 6's MFMA network end forms the last block's reduce sums
-# from a two-piece fp16 g1: <= 1.1 on the well-conditioned fixtures, 5.3 / 6.7 / 9.0 (f16x3 /
+# from a two-piece fp16 g1: <= 1.1 on the well-conditioned fixtures, 4.3 / 6.5 / 3.6 (f16x3 /
 # bf16x6 / fp32) on the saturated vae128_b2_edge, on decoder.13.0.  One fp32 run (round 5,
 # gpurun_out/t_sw1.txt) returned 180.8 on decoder.13.0 with a 200x weight-gradient error on the
 # same layer while the layers whose gradients flow through decoder.13's gy were exact: most
